@@ -1,0 +1,160 @@
+/*
+ * tfhe_gpu.h — C ABI of the MI355X TFHE gate-bootstrap engine.
+ *
+ * This is the drop-in boundary for zig-tfhe's bootstrap strategy plug point
+ * (src/bootstrap.zig:30-47, src/bootstrap/vanilla.zig:38-69, callers
+ * src/gates.zig:48-129).  A Zig `bootstrap/hip.zig` strategy would declare
+ * these functions `extern fn` and map a negative status to a Zig error
+ * (INTEGRATION.md shows the binding).  Plain pointers and sizes only; the
+ * library owns all device memory; one context = one HIP device (+ one stream).
+ *
+ * Layouts are the reference's in-memory layouts:
+ *   TLWELv0      = uint32_t[n+1]            (tlwe.zig:11-12, b is the last word)
+ *   TLWELv1      = uint32_t[N+1]            (tlwe.zig:243-244)
+ *   TRLWELv1     = uint32_t[2][N]  a then b (trlwe.zig:15-17)
+ *   BootstrappingKey  = double[n][2L][2][N] (key.zig:31, trgsw.zig:75-77,
+ *                        trlwe.zig:104-106: each N = re[N/2] ++ im[N/2])
+ *   KeySwitchingKey   = uint32_t[N*t*2^basebit][n+1]  (key.zig:28, :148-172)
+ * Status: 0 = OK, negative = error (tfhe_gpu_last_error has the text).
+ * Calls on one context are serialised by the caller (as the reference's
+ * single-threaded Gates); distinct contexts are independent.
+ */
+#ifndef TFHE_GPU_H
+#define TFHE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFHE_GPU_ABI_VERSION 1
+
+enum {
+    TFHE_OK = 0,
+    TFHE_ERR_INVALID = -1,     /* bad argument / unsupported parameter set      */
+    TFHE_ERR_HIP = -2,         /* HIP runtime error (no device, launch failure) */
+    TFHE_ERR_NO_KEY = -3,      /* bootstrap requested before a cloud key loaded */
+    TFHE_ERR_OOM = -4          /* device allocation failed                      */
+};
+
+/* Gate op codes — gates.zig:48-121 (pre-combination constants SURVEY §8a A2). */
+enum {
+    TFHE_GATE_NAND = 0, TFHE_GATE_OR = 1, TFHE_GATE_AND = 2, TFHE_GATE_XOR = 3,
+    TFHE_GATE_XNOR = 4, TFHE_GATE_NOR = 5, TFHE_GATE_ANDNY = 6, TFHE_GATE_ANDYN = 7,
+    TFHE_GATE_ORNY = 8, TFHE_GATE_ORYN = 9,
+    TFHE_GATE_COPY = 255       /* no pre-combination: bootstrap input a as is */
+};
+
+/* Runtime form of params.zig SecurityParams (:36-67).  N must be 1024. */
+typedef struct {
+    uint32_t n;        /* TLWE lv0 dimension (tlwe_lv0.n)   */
+    uint32_t N;        /* polynomial size (trgsw_lv1.n)     */
+    uint32_t nbit;     /* log2 N                             */
+    uint32_t L;        /* gadget levels                      */
+    uint32_t bgbit;    /* log2 Bg                            */
+    uint32_t basebit;  /* key-switch base bits               */
+    uint32_t iks_t;    /* key-switch levels                  */
+    uint32_t _pad;
+    double alpha_lv0;  /* tlwe_lv0.alpha                     */
+    double alpha_lv1;  /* trlwe_lv1.alpha                    */
+    double alpha_ksk;  /* KSK_ALPHA (params.zig:419-420)     */
+    double alpha_bsk;  /* BSK_ALPHA (params.zig:421-422)     */
+} tfhe_params;
+
+typedef struct tfhe_gpu_ctx tfhe_gpu_ctx;
+
+int         tfhe_gpu_abi_version(void);
+/* Context on HIP device `device`.  Replaces the implicit per-thread FFT plan
+ * (fft.zig:983-992) and owns the device copy of the CloudKey. */
+int         tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out);
+void        tfhe_gpu_destroy(tfhe_gpu_ctx *ctx);
+const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *ctx);
+int         tfhe_gpu_sync(tfhe_gpu_ctx *ctx);
+/* Run this context's work on a caller-owned hipStream_t (NULL = own stream). */
+int         tfhe_gpu_set_stream(tfhe_gpu_ctx *ctx, void *hip_stream);
+
+/* ---- Cloud key (key.zig:61-118) -------------------------------------- */
+/* Upload a CloudKey held in host memory in the reference layout
+ * (CloudKey.decomposition_offset, .blind_rotate_testvec, .bootstrapping_key
+ * .items, .key_switching_key.items).  bsk_len / ksk_len are element counts. */
+int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *ctx, uint32_t decomposition_offset,
+                            const uint32_t *testvec_a, const uint32_t *testvec_b,
+                            const double *bsk, size_t bsk_len,
+                            const uint32_t *ksk, size_t ksk_len);
+/* Generate SecretKey.new (key.zig:41-57) + CloudKey.new (key.zig:70-77) with
+ * a seeded RNG (Zig DefaultPrng restated; `seed` replaces getUniqueSeed()),
+ * FFTs on the device, and load it.  key_lv0/key_lv1 receive the secret key
+ * (n / N words); bsk_out / ksk_out (may be NULL) receive the host copy in the
+ * reference layout. */
+int tfhe_gpu_keygen(tfhe_gpu_ctx *ctx, uint64_t secret_seed, uint64_t cloud_seed,
+                    uint32_t *key_lv0, uint32_t *key_lv1, double *bsk_out, uint32_t *ksk_out);
+/* Device-resident key blob, for the one-time RCCL broadcast across ranks:
+ * export copies the context's device key into caller device buffers of the
+ * reported sizes; import loads a blob another context exported. */
+int tfhe_gpu_key_blob_bytes(const tfhe_gpu_ctx *ctx, size_t *bsk_bytes, size_t *ksk_bytes);
+int tfhe_gpu_export_key_device(tfhe_gpu_ctx *ctx, void *bsk_dev, void *ksk_dev,
+                               uint32_t *decomposition_offset, uint32_t *testvec /*2N host*/);
+int tfhe_gpu_import_key_device(tfhe_gpu_ctx *ctx, const void *bsk_dev, const void *ksk_dev,
+                               uint32_t decomposition_offset, const uint32_t *testvec /*2N host*/);
+
+/* ---- Bootstrap / gates (host buffers, synchronous) ---------------------- */
+/* VanillaBootstrap.bootstrap (vanilla.zig:38-52) over B TLWELv0. */
+int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, uint32_t *out, size_t B);
+/* Gates.*Gate (gates.zig:48-121): per-item op + pre-combination + bootstrap. */
+int tfhe_gpu_gate_batch(tfhe_gpu_ctx *ctx, const uint8_t *ops, const uint32_t *a,
+                        const uint32_t *b, uint32_t *out, size_t B);
+/* trgsw.blindRotate (trgsw.zig:290-333) / blindRotateWithTestvec (:336-400):
+ * testvec = NULL uses the cloud key's; out = B TRLWELv1. */
+int tfhe_gpu_blind_rotate_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, const uint32_t *testvec,
+                                uint32_t *trlwe_out, size_t B);
+/* Programmable bootstrap: blindRotateWithTestvec + sampleExtractIndex(0) +
+ * identityKeySwitching with a LUT test vector (lut/generator.zig:85-135). */
+int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, const uint32_t *testvec,
+                                 uint32_t *out, size_t B);
+
+/* ---- Same, on device-resident buffers (async on the context stream) ---- */
+int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *ctx, const uint8_t *ops_dev, const uint32_t *a_dev,
+                            const uint32_t *b_dev, uint32_t *out_dev, size_t B);
+int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *ctx, const uint32_t *in_dev, uint32_t *out_dev,
+                                 size_t B);
+
+/* ---- Stage entry points (parity tests; same kernels as the path) ------- */
+/* KlemsaProcessor.ifft1024 (fft.zig:293-366): B×N u32 -> B×N f64. */
+int tfhe_gpu_fft_forward_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, double *out, size_t B);
+/* KlemsaProcessor.fft1024 (fft.zig:370-443): B×N f64 -> B×N u32. */
+int tfhe_gpu_fft_inverse_batch(tfhe_gpu_ctx *ctx, const double *in, uint32_t *out, size_t B);
+/* KlemsaProcessor.poly_mul (fft.zig:458-492): B pairs. */
+int tfhe_gpu_poly_mul_batch(tfhe_gpu_ctx *ctx, const uint32_t *a, const uint32_t *b,
+                            uint32_t *out, size_t B);
+/* trgsw.externalProductWithFft (trgsw.zig:111-154) against BK row `bk_index`
+ * of the loaded key (or `trgsw_fft` = one TRGSWLv1FFT, 2L*2*N doubles, if non-NULL). */
+int tfhe_gpu_external_product_batch(tfhe_gpu_ctx *ctx, const double *trgsw_fft, uint32_t bk_index,
+                                    const uint32_t *trlwe_in, uint32_t *trlwe_out, size_t B);
+/* trgsw.identityKeySwitching (trgsw.zig:471-502): B TLWELv1 -> B TLWELv0. */
+int tfhe_gpu_key_switch_batch(tfhe_gpu_ctx *ctx, const uint32_t *in_lv1, uint32_t *out_lv0, size_t B);
+
+/* ---- Host-side TLWELv0 helpers (no device needed) ---------------------- */
+/* TLWELv0.encryptBool (tlwe.zig:52-55 -> encryptF64 :34-49); item i uses
+ * DefaultPrng(seed0 + i) in place of getUniqueSeed(). */
+int tfhe_encrypt_bool_batch(const tfhe_params *params, const uint32_t *key_lv0, const uint8_t *bits,
+                            uint64_t seed0, uint32_t *out, size_t B);
+/* TLWELv0.decryptBool (tlwe.zig:58-68). */
+int tfhe_decrypt_bool_batch(const tfhe_params *params, const uint32_t *key_lv0, const uint32_t *ct,
+                            uint8_t *bits, size_t B);
+/* encryptLweMessage / decryptLweMessage (tlwe.zig:74-117), message modulus m. */
+int tfhe_encrypt_lwe_message_batch(const tfhe_params *params, const uint32_t *key_lv0,
+                                   const uint32_t *msgs, uint32_t m, uint64_t seed0, uint32_t *out,
+                                   size_t B);
+int tfhe_decrypt_lwe_message_batch(const tfhe_params *params, const uint32_t *key_lv0,
+                                   const uint32_t *ct, uint32_t m, uint32_t *msgs, size_t B);
+/* Generator.generateLookupTableAssign (lut/generator.zig:85-135): testvec
+ * (2N words, a = 0) for f given as a table f_table[x], x < m. */
+int tfhe_lut_generate(const tfhe_params *params, uint32_t m, const uint32_t *f_table,
+                      uint32_t *testvec);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TFHE_GPU_H */

@@ -1,0 +1,112 @@
+"""Generates the committed fixtures in tests/golden/ (run from the repo root).
+
+The reference (Zig) cannot be built or run in this image and ships no golden
+vectors for this path, so the fixtures are of two kinds:
+
+* independent exact values, computed here WITHOUT the oracle:
+  - twiddles.npz: the reference's twist factors cos/sin(i*pi/1024) (fft.zig:98-106)
+    evaluated by the platform libm (glibc, via Python's math module) and
+    correctly rounded by mpmath (200 bits); the stage-twiddle recurrence of
+    radix2FFT (fft.zig:590-616) restated in Python floats (IEEE doubles).
+  - polymul_bigint.npz: exact negacyclic products mod 2^32 by Python big ints.
+* oracle regression vectors (oracle_vectors.npz): seeded inputs and the
+  oracle's outputs for the FFT pair and a small gate batch, so the GPU tests
+  have fixed expected bits even before the oracle is rebuilt on a box.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+
+
+def twiddles():
+    import mpmath
+    mpmath.mp.prec = 200
+    N = 1024
+    unit = math.pi / N
+    re_g, im_g, re_c, im_c = [], [], [], []
+    for i in range(N // 2):
+        ang = float(i) * unit  # one f64 rounding, like the reference
+        re_g.append(math.cos(ang))
+        im_g.append(math.sin(ang))
+        a = mpmath.mpf(ang)
+        re_c.append(float(mpmath.cos(a)))
+        im_c.append(float(mpmath.sin(a)))
+    fr, fi = [0.0] * (N // 2 - 1), [0.0] * (N // 2 - 1)
+    n = N // 2
+    ln = 2
+    while ln <= n:
+        ang = -2.0 * math.pi / ln
+        wr, wi = math.cos(ang), math.sin(ang)
+        w_re, w_im = 1.0, 0.0
+        for j in range(ln // 2):
+            fr[ln // 2 - 1 + j], fi[ln // 2 - 1 + j] = w_re, w_im
+            t = w_re * wr - w_im * wi
+            w_im = w_re * wi + w_im * wr
+            w_re = t
+        ln *= 2
+    np.savez(os.path.join(HERE, "twiddles.npz"),
+             twist_re_glibc=np.array(re_g), twist_im_glibc=np.array(im_g),
+             twist_re_cr=np.array(re_c), twist_im_cr=np.array(im_c),
+             stage_fwd_re=np.array(fr), stage_fwd_im=np.array(fi))
+    diff = [(i, "cos") for i in range(N // 2) if re_g[i] != re_c[i]] + \
+           [(i, "sin") for i in range(N // 2) if im_g[i] != im_c[i]]
+    print("twist entries where libm != correctly rounded:", diff)
+
+
+def polymul_bigint(count=3):
+    g = np.random.default_rng(2024)
+    A, B, E = [], [], []
+    for _ in range(count):
+        a = g.integers(0, 1 << 32, 1024, dtype=np.uint64).astype(np.uint32)
+        b = (g.integers(0, 1 << 32, 1024, dtype=np.uint64) % 64).astype(np.uint32)
+        ai, bi = [int(x) for x in a], [int(x) for x in b]
+        res = [0] * 1024
+        for i in range(1024):
+            x = ai[i]
+            for j in range(1024):
+                k = i + j
+                if k < 1024:
+                    res[k] += x * bi[j]
+                else:
+                    res[k - 1024] -= x * bi[j]
+        A.append(a)
+        B.append(b)
+        E.append(np.array([v % (1 << 32) for v in res], np.uint32))
+    np.savez(os.path.join(HERE, "polymul_bigint.npz"), a=np.array(A), b=np.array(B), exact=np.array(E))
+
+
+def oracle_vectors():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle, params
+    o = Oracle()
+    g = np.random.default_rng(77)
+    polys = g.integers(0, 1 << 32, (6, 1024), dtype=np.uint64).astype(np.uint32)
+    polys[0] = 0
+    polys[1] = 0xFFFFFFFF
+    polys[2] = 0
+    polys[2][0] = 1 << 31
+    polys[3] = 0x7FFFFFFF
+    fwd = np.array([o.ifft(x) for x in polys])
+    inv = np.array([o.fft(f) for f in fwd])
+    p = params("80")
+    k0, k1 = o.secret_key(p, 42)
+    ck = o.cloud_key(p, 43, k0, k1)
+    ops = np.arange(10, dtype=np.uint8)
+    bits_a = g.integers(0, 2, 10)
+    bits_b = g.integers(0, 2, 10)
+    A = np.array([o.tlwe_encrypt_bool(p.n, a, p.alpha_lv0, k0, 7000 + i) for i, a in enumerate(bits_a)])
+    B = np.array([o.tlwe_encrypt_bool(p.n, b, p.alpha_lv0, k0, 8000 + i) for i, b in enumerate(bits_b)])
+    out = o.gate_batch(p, ops, A, B, ck, threads=8)
+    np.savez(os.path.join(HERE, "oracle_vectors.npz"), fft_in=polys, fft_fwd=fwd, fft_inv=inv,
+             gate_ops=ops, gate_a=A, gate_b=B, gate_out=out, gate_params="80", sk_seed=42, ck_seed=43)
+
+
+if __name__ == "__main__":
+    twiddles()
+    polymul_bigint()
+    oracle_vectors()

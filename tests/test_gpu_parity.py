@@ -1,0 +1,230 @@
+"""GPU parity tests: every stage of the MI355X path, through the C ABI,
+bit-exact against the CPU oracle (oracle/tfhe_oracle.c) on the same seeded
+inputs, plus size-independent properties at full batch size.
+
+Bit-exact means equal u32 words; for the f64 FFT stage it means equal f64
+values (+0.0 == -0.0: signs of zero never reach an output integer).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import tfhe_amd
+from conftest import get_keys, rng
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def u32rand(g, *shape):
+    return g.integers(0, 1 << 32, shape, dtype=np.uint64).astype(np.uint32)
+
+
+_CTX = {}
+
+
+def ctx_for(oracle, pname):
+    """Context with the oracle's seeded cloud key loaded (sk 42, ck 43)."""
+    if pname not in _CTX:
+        k = get_keys(oracle, pname)
+        c = tfhe_amd.Context(pname, 0)
+        c.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+        _CTX[pname] = (c, k)
+    return _CTX[pname]
+
+
+# ---- FFT (fft.zig:293-443) -------------------------------------------------
+def test_fft_forward_golden_and_random(oracle):
+    c, _ = ctx_for(oracle, "80")
+    g = np.load(os.path.join(GOLDEN, "oracle_vectors.npz"))
+    assert np.array_equal(c.fft_forward(g["fft_in"]), g["fft_fwd"])
+    x = u32rand(rng(1), 64, 1024)
+    want = np.array([oracle.ifft(p) for p in x])
+    assert np.array_equal(c.fft_forward(x), want)
+
+
+def test_fft_inverse_golden_and_random(oracle):
+    c, _ = ctx_for(oracle, "80")
+    g = np.load(os.path.join(GOLDEN, "oracle_vectors.npz"))
+    assert np.array_equal(c.fft_inverse(g["fft_fwd"]), g["fft_inv"])
+    # MAC-like spectra: sums of products of digits and key spectra
+    f = rng(2).normal(0, 2.0 ** 40, (64, 1024))
+    want = np.array([oracle.fft(v) for v in f])
+    assert np.array_equal(c.fft_inverse(f), want)
+
+
+@pytest.mark.parametrize("small_b", [True, False])
+def test_poly_mul(oracle, small_b):  # fft.zig:458-492
+    c, _ = ctx_for(oracle, "80")
+    g = rng(3)
+    a = u32rand(g, 32, 1024)
+    b = u32rand(g, 32, 1024)
+    if small_b:
+        b %= 64
+    want = np.array([oracle.poly_mul(x, y) for x, y in zip(a, b)])
+    assert np.array_equal(c.poly_mul(a, b), want)
+
+
+# ---- external product / key switch (trgsw.zig) -----------------------------
+@pytest.mark.parametrize("pname", ["128", "uint4"])
+def test_external_product_vs_oracle(oracle, pname):
+    c, k = ctx_for(oracle, pname)
+    p = k.p
+    g = rng(4)
+    x = u32rand(g, 8, 2048)
+    trgsw = oracle.trgsw_encrypt_torus_fft(p, 1, p.alpha_bsk, k.k1, 17)
+    want = np.array([oracle.external_product(p, trgsw, t, k.ck.offset) for t in x])
+    assert np.array_equal(c.external_product(x, trgsw_fft=trgsw), want)
+    # against a row of the resident key
+    want = np.array([oracle.external_product(p, k.ck.bk[5], t, k.ck.offset) for t in x])
+    assert np.array_equal(c.external_product(x, bk_index=5), want)
+
+
+@pytest.mark.parametrize("pname,B", [("128", 9), ("80", 1), ("uint4", 17)])
+def test_key_switch_vs_oracle(oracle, pname, B):
+    c, k = ctx_for(oracle, pname)
+    lv1 = u32rand(rng(5), B, 1025)
+    want = np.array([oracle.identity_key_switch(k.p, v, k.ck.ksk) for v in lv1])
+    assert np.array_equal(c.key_switch(lv1), want)
+
+
+# ---- blind rotation / bootstrap ---------------------------------------------
+@pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
+def test_blind_rotate_vs_oracle(oracle, pname, B):
+    c, k = ctx_for(oracle, pname)
+    cts = u32rand(rng(6), B, k.p.n + 1)  # uniform TLWE: bit-exactness only
+    want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
+    assert np.array_equal(c.blind_rotate_batch(cts), want)
+
+
+def test_gate_golden_vectors(oracle):
+    """All ten reference gates, committed inputs/outputs (80-bit, seeds 42/43)."""
+    c, _ = ctx_for(oracle, "80")
+    g = np.load(os.path.join(GOLDEN, "oracle_vectors.npz"))
+    assert np.array_equal(c.gate_batch(g["gate_ops"], g["gate_a"], g["gate_b"]), g["gate_out"])
+
+
+def test_gates_128_all_ops_bit_exact(oracle):
+    c, k = ctx_for(oracle, "128")
+    p = k.p
+    g = rng(7)
+    ops = np.repeat(np.arange(10, dtype=np.uint8), 2)
+    A = np.array([oracle.tlwe_encrypt_bool(p.n, int(b), p.alpha_lv0, k.k0, 100 + i)
+                  for i, b in enumerate(g.integers(0, 2, ops.size))])
+    B = np.array([oracle.tlwe_encrypt_bool(p.n, int(b), p.alpha_lv0, k.k0, 200 + i)
+                  for i, b in enumerate(g.integers(0, 2, ops.size))])
+    want = oracle.gate_batch(p, ops, A, B, k.ck, threads=8)
+    got = c.gate_batch(ops, A, B)
+    assert np.array_equal(got, want)
+    # and the same through the Gates mirror
+    gates = tfhe_amd.Gates(c)
+    assert np.array_equal(gates.nand_gate(A[:1], B[:1]), oracle.gate_batch(p, ops[:1] * 0, A[:1], B[:1], k.ck)[0])
+
+
+def test_bootstrap_edge_rotations(oracle):
+    """a~ in {0, 2N} (skipped CMUX), b near the 2^32 wrap, empty and single batches."""
+    c, k = ctx_for(oracle, "80")
+    p = k.p
+    cts = u32rand(rng(8), 4, p.n + 1)
+    cts[0, : p.n // 2] = 0                      # a~ = 0
+    cts[1, : p.n // 2] = 0xFFFFFFFF             # a~ = 2048 (64-bit add, no wrap)
+    cts[1, p.n] = 0xFFFFFFFF                    # b~ = 0
+    cts[2, p.n] = (1 << 20) - 1                 # b~ = 2N exactly
+    cts[3, ::2] = 0xFFF00000                    # a~ = 2048 boundary (0xFFF00000 + 2^20 = 2^32)
+    want = np.array([oracle.bootstrap(p, t, k.ck) for t in cts])
+    assert np.array_equal(c.bootstrap_batch(cts), want)
+    assert c.bootstrap_batch(np.zeros((0, p.n + 1), np.uint32)).shape == (0, p.n + 1)
+    assert np.array_equal(c.bootstrap_batch(cts[:1]), want[:1])
+
+
+def test_nand_batch_1024_128bit(oracle):
+    """BASELINE config 2 shape: 1024 NAND, 128-bit; truth table for all, bits for a sample."""
+    c, k = ctx_for(oracle, "128")
+    p = k.p
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    g = rng(9)
+    a_bits = g.integers(0, 2, 1024).astype(np.uint8)
+    b_bits = g.integers(0, 2, 1024).astype(np.uint8)
+    A = sk.encrypt_bool(a_bits, seed0=10_000)
+    B = sk.encrypt_bool(b_bits, seed0=20_000)
+    out = c.gate_batch(np.zeros(1024, np.uint8), A, B)
+    assert np.array_equal(sk.decrypt_bool(out), ~(a_bits.astype(bool) & b_bits.astype(bool)))
+    idx = g.choice(1024, 6, replace=False)
+    want = oracle.gate_batch(p, np.zeros(idx.size, np.uint8), A[idx], B[idx], k.ck, threads=6)
+    assert np.array_equal(out[idx], want)
+    # determinism
+    assert np.array_equal(c.gate_batch(np.zeros(64, np.uint8), A[:64], B[:64]), out[:64])
+
+
+def test_lut_pbs_uint4(oracle):
+    """BASELINE config 5 semantics: f(x) = (x+1) mod 16 over all 16 messages."""
+    c, k = ctx_for(oracle, "uint4")
+    p = k.p
+    f = lambda x: (x + 1) % 16
+    tv = tfhe_amd.lut_generate(c.params, 16, f)
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    msgs = np.tile(np.arange(16, dtype=np.uint32), 2)
+    cts = sk.encrypt_lwe_message(msgs, 16, seed0=77)
+    out = c.bootstrap_lut_batch(cts, tv)
+    want = np.array([oracle.gate_batch(p, np.array([255], np.uint8), t[None], t[None], k.ck, testvec=tv)[0]
+                     for t in cts[:4]])
+    assert np.array_equal(out[:4], want)
+    assert np.array_equal(sk.decrypt_lwe_message(out, 16), (msgs + 1) % 16)
+
+
+def test_keygen_matches_oracle(oracle):
+    """tfhe_gpu_keygen (host RNG + device FFTs) == oracle CloudKey.new, bit for bit."""
+    p = get_keys(oracle, "80").p
+    c = tfhe_amd.Context("80", 0)
+    sk, (bk, ksk) = c.keygen(42, 43, want_host_copy=True)
+    k0, k1 = oracle.secret_key(p, 42)
+    assert np.array_equal(sk.key_lv0, k0) and np.array_equal(sk.key_lv1, k1)
+    ck = oracle.cloud_key(p, 43, k0, k1)
+    assert np.array_equal(ksk, ck.ksk)
+    assert np.array_equal(bk, ck.bk)
+    c.close()
+
+
+@pytest.mark.slow
+def test_add_two_numbers_gpu(oracle):
+    """examples/add_two_numbers.zig: 16-bit ripple-carry, 402 + 304 = 706."""
+    c, k = ctx_for(oracle, "128")
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    gates = tfhe_amd.Gates(c)
+    A = sk.encrypt_bool([(402 >> i) & 1 for i in range(16)], seed0=1)
+    Bc = sk.encrypt_bool([(304 >> i) & 1 for i in range(16)], seed0=101)
+    carry = sk.encrypt_bool([0], seed0=999)[0]
+    bits = []
+    for i in range(16):
+        x = gates.xor_gate(A[i], Bc[i])
+        ab = gates.and_gate(A[i], Bc[i])
+        xc = gates.and_gate(x, carry)
+        bits.append(gates.xor_gate(x, carry))
+        carry = gates.or_gate(ab, xc)
+    val = sum(int(b) << i for i, b in enumerate(sk.decrypt_bool(np.array(bits))))
+    assert val == 706
+
+
+def test_device_resident_api_with_torch(oracle):
+    """tfhe_gpu_gate_batch_dev on torch-allocated HBM buffers and torch's stream."""
+    torch = pytest.importorskip("torch")
+    c, k = ctx_for(oracle, "80")
+    p = k.p
+    g = rng(11)
+    ops = np.arange(10, dtype=np.uint8)
+    A = u32rand(g, 10, p.n + 1)
+    B = u32rand(g, 10, p.n + 1)
+    want = c.gate_batch(ops, A, B)
+    dev = torch.device("cuda", 0)
+    t_ops = torch.from_numpy(ops).to(dev)
+    t_a = torch.from_numpy(A.view(np.int32)).to(dev)
+    t_b = torch.from_numpy(B.view(np.int32)).to(dev)
+    t_o = torch.zeros_like(t_a)
+    c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    try:
+        c.gate_batch_dev(t_ops.data_ptr(), t_a.data_ptr(), t_b.data_ptr(), t_o.data_ptr(), 10)
+        torch.cuda.synchronize(dev)
+    finally:
+        c.set_stream(None)
+    assert np.array_equal(t_o.cpu().numpy().view(np.uint32), want)

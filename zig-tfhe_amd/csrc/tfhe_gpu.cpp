@@ -1,0 +1,600 @@
+// tfhe_gpu.cpp — C-ABI implementation (include/tfhe_gpu.h): contexts, device
+// key residency, batch entry points and seeded key generation.  Host code;
+// all bootstrap arithmetic runs in tfhe_kernels.hip.
+#include "tfhe_gpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "host_math.hpp"
+#include "tfhe_internal.hpp"
+
+using namespace tfhe;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct tfhe_gpu_ctx {
+    tfhe_params P{};
+    KParams K{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    std::string err;
+    // constant tables
+    C2 *d_twist = nullptr, *d_tw = nullptr;
+    // cloud key
+    bool has_key = false;
+    uint32_t offset = 0;
+    std::vector<uint32_t> testvec;  // host copy, 2N
+    uint32_t *d_testvec = nullptr;  // cloud testvec (2N)
+    double *d_bk = nullptr;         // device layout, n*2L*512 double4
+    uint32_t *d_ksk = nullptr;      // reference layout
+    size_t bk_bytes = 0, ksk_bytes = 0;
+    // scratch, grown on demand
+    DevBuf s_a, s_b, s_out, s_lv1, s_ops, s_tv, s_tmp;
+};
+
+namespace {
+
+int fail(tfhe_gpu_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(tfhe_gpu_ctx *c, hipError_t e, const char *where) {
+    return fail(c, TFHE_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(c, expr)                                         \
+    do {                                                        \
+        hipError_t _e = (expr);                                 \
+        if (_e != hipSuccess) return hip_fail((c), _e, #expr);  \
+    } while (0)
+
+bool params_ok(const tfhe_params *p, std::string &why) {
+    if (!p) { why = "params is NULL"; return false; }
+    if (p->N != 1024 || p->nbit != 10) { why = "only N=1024 (nbit=10) is supported"; return false; }
+    if (p->n == 0 || p->n > 1024) { why = "n must be in [1, 1024]"; return false; }
+    if (p->L < 1 || p->L > 3) { why = "L must be 1, 2 or 3"; return false; }
+    if (p->bgbit < 1 || p->bgbit * p->L > 32) { why = "bgbit*L must be <= 32"; return false; }
+    if (p->basebit < 1 || p->basebit > 8 || p->iks_t < 1 || p->basebit * p->iks_t >= 31) {
+        why = "unsupported key-switch base/levels";
+        return false;
+    }
+    return true;
+}
+
+int ensure(tfhe_gpu_ctx *c, DevBuf &b, size_t bytes) {
+    if (b.bytes >= bytes) return TFHE_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    b.bytes = want;
+    return TFHE_OK;
+}
+
+DevTables tables(const tfhe_gpu_ctx *c) { return DevTables{c->d_twist, c->d_tw}; }
+
+size_t tlwe0_words(const tfhe_gpu_ctx *c) { return (size_t)c->P.n + 1; }
+size_t bk_rows(const tfhe_params &p) { return (size_t)p.n * 2 * p.L; }
+size_t ksk_words(const tfhe_params &p) { return (size_t)p.N * p.iks_t * (1u << p.basebit) * (p.n + 1); }
+
+int set_key_common(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv_a, const uint32_t *tv_b) {
+    const uint32_t N = c->P.N;
+    c->offset = offset;
+    c->K.offset = offset;
+    c->testvec.assign(tv_a, tv_a + N);
+    c->testvec.insert(c->testvec.end(), tv_b, tv_b + N);
+    if (!c->d_testvec) HIPCHK(c, hipMalloc((void **)&c->d_testvec, sizeof(uint32_t) * 2 * N));
+    HIPCHK(c, hipMemcpyAsync(c->d_testvec, c->testvec.data(), sizeof(uint32_t) * 2 * N, hipMemcpyHostToDevice,
+                             c->stream));
+    if (!c->d_bk) {
+        c->bk_bytes = bk_rows(c->P) * 2048 * sizeof(double);
+        c->ksk_bytes = ksk_words(c->P) * sizeof(uint32_t);
+        hipError_t e = hipMalloc((void **)&c->d_bk, c->bk_bytes);
+        if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, "hipMalloc(bk)");
+        e = hipMalloc((void **)&c->d_ksk, c->ksk_bytes);
+        if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, "hipMalloc(ksk)");
+    }
+    return TFHE_OK;
+}
+
+// Blind rotation (+ optional key switch) over device buffers, async.
+int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b,
+                      const uint32_t *testvec_dev, uint32_t *out, size_t B, bool key_switch) {
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    if (B == 0) return TFHE_OK;
+    int rc = ensure(c, c->s_lv1, B * 1025 * sizeof(uint32_t));
+    if (rc) return rc;
+    uint32_t *lv1 = key_switch ? (uint32_t *)c->s_lv1.p : out;
+    HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
+                                  lv1, key_switch ? BR_OUT_LV1 : BR_OUT_TRLWE, B, c->stream));
+    if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream));
+    return TFHE_OK;
+}
+
+int h2d(tfhe_gpu_ctx *c, DevBuf &buf, const void *src, size_t bytes) {
+    int rc = ensure(c, buf, bytes);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return TFHE_OK;
+}
+
+int d2h_sync(tfhe_gpu_ctx *c, void *dst, const void *src, size_t bytes) {
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TFHE_OK;
+}
+
+// TLWELv0.encryptF64 (tlwe.zig:34-49) with DefaultPrng(seed).
+void tlwe_encrypt(uint32_t n, double mu, double alpha, const uint32_t *key, uint64_t seed, uint32_t *out) {
+    host::Rng r(seed);
+    uint32_t inner = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t x = r.u32();
+        inner += key[i] * x;
+        out[i] = x;
+    }
+    host::NormalDist nd(0.0, alpha);
+    uint32_t mu_t = host::f64_to_torus(mu);
+    out[n] = inner + host::gaussian_torus(mu_t, nd, r);
+}
+
+uint32_t tlwe_phase(uint32_t n, const uint32_t *ct, const uint32_t *key) {
+    uint32_t inner = 0;
+    for (uint32_t i = 0; i < n; i++) inner += ct[i] * key[i];
+    return ct[n] - inner;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfhe_gpu_abi_version(void) { return TFHE_GPU_ABI_VERSION; }
+
+int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
+    if (!out) return TFHE_ERR_INVALID;
+    *out = nullptr;
+    std::string why;
+    if (!params_ok(params, why)) {
+        std::fprintf(stderr, "tfhe_gpu_create: %s\n", why.c_str());
+        return TFHE_ERR_INVALID;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return TFHE_ERR_HIP;
+    auto *c = new tfhe_gpu_ctx();
+    c->P = *params;
+    c->device = device;
+    c->K = KParams{(int)params->n, (int)params->N, (int)params->L, (int)params->bgbit, (int)params->basebit,
+                   (int)params->iks_t, 0};
+    int rc = TFHE_OK;
+    do {
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) { rc = hip_fail(c, e, "hipSetDevice"); break; }
+        e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+        if (e != hipSuccess) { rc = hip_fail(c, e, "hipStreamCreate"); break; }
+        c->stream = c->own_stream;
+        // FFT constant tables (fft.zig:92-106 twists, :590-616 recurrence)
+        std::vector<double> tre, tim, fre, fim, ire, iim;
+        host::twist_table(params->N, tre, tim);
+        host::stage_twiddles(params->N, false, fre, fim);
+        host::stage_twiddles(params->N, true, ire, iim);
+        // the inverse kernels use conj(forward): that must equal the
+        // inverse recurrence bit for bit (glibc sin is odd, cos even)
+        for (size_t i = 0; i < fre.size(); i++)
+            if (std::memcmp(&fre[i], &ire[i], 8) != 0 || -fim[i] != iim[i]) {
+                rc = fail(c, TFHE_ERR_INVALID, "inverse twiddle table is not the conjugate of the forward one");
+                break;
+            }
+        if (rc) break;
+        std::vector<C2> tw2(tre.size()), st2(fre.size());
+        for (size_t i = 0; i < tre.size(); i++) tw2[i] = C2{tre[i], tim[i]};
+        for (size_t i = 0; i < fre.size(); i++) st2[i] = C2{fre[i], fim[i]};
+        if (hipMalloc((void **)&c->d_twist, sizeof(C2) * tw2.size()) != hipSuccess ||
+            hipMalloc((void **)&c->d_tw, sizeof(C2) * st2.size()) != hipSuccess) {
+            rc = fail(c, TFHE_ERR_OOM, "hipMalloc(tables)");
+            break;
+        }
+        e = hipMemcpy(c->d_twist, tw2.data(), sizeof(C2) * tw2.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(c->d_tw, st2.data(), sizeof(C2) * st2.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { rc = hip_fail(c, e, "upload tables"); break; }
+    } while (0);
+    if (rc != TFHE_OK) {
+        std::fprintf(stderr, "tfhe_gpu_create: %s\n", c->err.c_str());
+        tfhe_gpu_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return TFHE_OK;
+}
+
+void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (void *p : {(void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
+                    c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p})
+        if (p) (void)hipFree(p);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int tfhe_gpu_sync(tfhe_gpu_ctx *c) {
+    if (!c) return TFHE_ERR_INVALID;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TFHE_OK;
+}
+
+int tfhe_gpu_set_stream(tfhe_gpu_ctx *c, void *s) {
+    if (!c) return TFHE_ERR_INVALID;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return TFHE_OK;
+}
+
+int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv_a, const uint32_t *tv_b,
+                            const double *bsk, size_t bsk_len, const uint32_t *ksk, size_t ksk_len) {
+    if (!c || !tv_a || !tv_b || !bsk || !ksk) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t rows = bk_rows(c->P);
+    if (bsk_len != rows * 2 * c->P.N) return fail(c, TFHE_ERR_INVALID, "bsk_len != n*2L*2*N");
+    if (ksk_len != ksk_words(c->P)) return fail(c, TFHE_ERR_INVALID, "ksk_len != N*t*2^basebit*(n+1)");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = set_key_common(c, offset, tv_a, tv_b);
+    if (rc) return rc;
+    rc = h2d(c, c->s_tmp, bsk, bsk_len * sizeof(double));
+    if (rc) return rc;
+    HIPCHK(c, launch_bk_permute(c->K, (const double *)c->s_tmp.p, c->d_bk, rows, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk, c->ksk_bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_key = true;
+    return TFHE_OK;
+}
+
+int tfhe_gpu_key_blob_bytes(const tfhe_gpu_ctx *c, size_t *bsk_bytes, size_t *ksk_bytes) {
+    if (!c || !bsk_bytes || !ksk_bytes) return TFHE_ERR_INVALID;
+    *bsk_bytes = bk_rows(c->P) * 2048 * sizeof(double);
+    *ksk_bytes = ksk_words(c->P) * sizeof(uint32_t);
+    return TFHE_OK;
+}
+
+int tfhe_gpu_export_key_device(tfhe_gpu_ctx *c, void *bsk_dev, void *ksk_dev, uint32_t *offset,
+                               uint32_t *testvec) {
+    if (!c || !bsk_dev || !ksk_dev) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(bsk_dev, c->d_bk, c->bk_bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ksk_dev, c->d_ksk, c->ksk_bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (offset) *offset = c->offset;
+    if (testvec) std::memcpy(testvec, c->testvec.data(), sizeof(uint32_t) * 2 * c->P.N);
+    return TFHE_OK;
+}
+
+int tfhe_gpu_import_key_device(tfhe_gpu_ctx *c, const void *bsk_dev, const void *ksk_dev, uint32_t offset,
+                               const uint32_t *testvec) {
+    if (!c || !bsk_dev || !ksk_dev || !testvec) return fail(c, TFHE_ERR_INVALID, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = set_key_common(c, offset, testvec, testvec + c->P.N);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_bk, bsk_dev, c->bk_bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk_dev, c->ksk_bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_key = true;
+    return TFHE_OK;
+}
+
+// SecretKey.new + CloudKey.new, seeded.  Host: every RNG draw in reference
+// order; device: the FFT-based poly_mul of each TRLWE encryption
+// (trlwe.zig:56-61) and the TRGSWLv1FFT forward transforms (trgsw.zig:81-91).
+int tfhe_gpu_keygen(tfhe_gpu_ctx *c, uint64_t secret_seed, uint64_t cloud_seed, uint32_t *key_lv0,
+                    uint32_t *key_lv1, double *bsk_out, uint32_t *ksk_out) {
+    if (!c || !key_lv0 || !key_lv1) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const tfhe_params &p = c->P;
+    const uint32_t N = p.N, n = p.n, L = p.L, T = p.iks_t, base = 1u << p.basebit;
+    HIPCHK(c, hipSetDevice(c->device));
+    {  // SecretKey.new (key.zig:41-57)
+        host::Rng r(secret_seed);
+        for (uint32_t i = 0; i < n; i++) key_lv0[i] = r.boolean() ? 1u : 0u;
+        for (uint32_t i = 0; i < N; i++) key_lv1[i] = r.boolean() ? 1u : 0u;
+    }
+    host::Rng master(cloud_seed);
+    // genKeySwitchingKey (key.zig:148-172): k = 0 rows are zeroed
+    std::vector<uint32_t> ksk(ksk_words(p), 0u);
+    for (uint32_t i = 0; i < N; i++)
+        for (uint32_t j = 0; j < T; j++)
+            for (uint32_t k = 1; k < base; k++) {
+                size_t idx = (size_t)base * T * i + (size_t)base * j + k;
+                uint32_t shift = (j + 1) * p.basebit;
+                double pv = ((double)k * (double)key_lv1[i]) / (double)(1u << shift);
+                tlwe_encrypt(n, pv, p.alpha_ksk, key_lv0, master.next(), ksk.data() + idx * (n + 1));
+            }
+    // genBootstrappingKey (key.zig:175-212): per i, TRGSW encryptTorus of
+    // key_lv0[i]: 2L TRLWE encryptions of zero (trlwe.zig:30-64), gadget on
+    // a[0] of row l / b[0] of row L+l.
+    const size_t R = bk_rows(p);  // n*2L TRLWE rows
+    std::vector<uint32_t> rows(R * 2 * N);
+    std::vector<uint32_t> noise(R * N);
+    for (size_t row = 0; row < R; row++) {
+        host::Rng r(master.next());
+        uint32_t *a = rows.data() + row * 2 * N;
+        for (uint32_t x = 0; x < N; x++) a[x] = r.u32();
+        host::NormalDist nd(0.0, p.alpha_bsk);
+        for (uint32_t x = 0; x < N; x++) noise[row * N + x] = host::gaussian_torus(0u, nd, r);
+    }
+    int rc = h2d(c, c->s_b, key_lv1, N * sizeof(uint32_t));
+    if (rc) return rc;
+    rc = ensure(c, c->s_out, R * N * sizeof(uint32_t));
+    if (rc) return rc;
+    // a*s for all rows: a_i lives at stride 2N inside `rows`
+    std::vector<uint32_t> a_only(R * N);
+    for (size_t row = 0; row < R; row++)
+        std::memcpy(a_only.data() + row * N, rows.data() + row * 2 * N, N * sizeof(uint32_t));
+    rc = h2d(c, c->s_a, a_only.data(), a_only.size() * sizeof(uint32_t));
+    if (rc) return rc;
+    HIPCHK(c, launch_poly_mul(tables(c), (const uint32_t *)c->s_a.p, (const uint32_t *)c->s_b.p, 0,
+                              (uint32_t *)c->s_out.p, R, c->stream));
+    std::vector<uint32_t> as(R * N);
+    rc = d2h_sync(c, as.data(), c->s_out.p, as.size() * sizeof(uint32_t));
+    if (rc) return rc;
+    for (size_t row = 0; row < R; row++) {
+        uint32_t *b = rows.data() + row * 2 * N + N;
+        for (uint32_t x = 0; x < N; x++) b[x] = noise[row * N + x] + as[row * N + x];
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t mu = key_lv0[i];
+        for (uint32_t l = 0; l < L; l++) {
+            uint32_t h = host::f64_to_torus(std::ldexp(1.0, -(int)((l + 1) * p.bgbit)));
+            rows[((size_t)i * 2 * L + l) * 2 * N] += mu * h;              // trlwe[l].a[0]
+            rows[((size_t)i * 2 * L + L + l) * 2 * N + N] += mu * h;      // trlwe[L+l].b[0]
+        }
+    }
+    // TRGSWLv1FFT.new: ifft of every a and b polynomial -> reference BK layout
+    rc = h2d(c, c->s_a, rows.data(), rows.size() * sizeof(uint32_t));
+    if (rc) return rc;
+    rc = ensure(c, c->s_tmp, R * 2 * N * sizeof(double));
+    if (rc) return rc;
+    HIPCHK(c, launch_fft_forward(tables(c), (const uint32_t *)c->s_a.p, (double *)c->s_tmp.p, R * 2, c->stream));
+    std::vector<uint32_t> tv(2 * N);
+    for (uint32_t x = 0; x < N; x++) {  // genTestvec (key.zig:134-145)
+        tv[x] = 0;
+        tv[N + x] = host::f64_to_torus(0.125);
+    }
+    uint32_t offset = 0;  // genDecompositionOffset (key.zig:121-131)
+    for (uint32_t l = 0; l < L; l++) offset += ((1u << p.bgbit) / 2) * (1u << (32 - (l + 1) * p.bgbit));
+    rc = set_key_common(c, offset, tv.data(), tv.data() + N);
+    if (rc) return rc;
+    HIPCHK(c, launch_bk_permute(c->K, (const double *)c->s_tmp.p, c->d_bk, R, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk.data(), c->ksk_bytes, hipMemcpyHostToDevice, c->stream));
+    if (bsk_out)
+        HIPCHK(c, hipMemcpyAsync(bsk_out, c->s_tmp.p, R * 2 * N * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ksk_out) std::memcpy(ksk_out, ksk.data(), c->ksk_bytes);
+    c->has_key = true;
+    return TFHE_OK;
+}
+
+int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
+    if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = h2d(c, c->s_a, in, B * w * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * w * 4);
+    if (!rc) rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, nullptr, (uint32_t *)c->s_out.p, B, true);
+    if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
+    return rc;
+}
+
+int tfhe_gpu_gate_batch(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b, uint32_t *out,
+                        size_t B) {
+    if (!c || (B && (!ops || !a || !b || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    for (size_t i = 0; i < B; i++)
+        if (ops[i] > TFHE_GATE_ORYN && ops[i] != TFHE_GATE_COPY) return fail(c, TFHE_ERR_INVALID, "bad gate op");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = h2d(c, c->s_ops, ops, B);
+    if (!rc) rc = h2d(c, c->s_a, a, B * w * 4);
+    if (!rc) rc = h2d(c, c->s_b, b, B * w * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * w * 4);
+    if (!rc)
+        rc = run_bootstrap_dev(c, (const uint8_t *)c->s_ops.p, (const uint32_t *)c->s_a.p, (const uint32_t *)c->s_b.p,
+                               nullptr, (uint32_t *)c->s_out.p, B, true);
+    if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
+    return rc;
+}
+
+int tfhe_gpu_blind_rotate_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *trlwe_out,
+                                size_t B) {
+    if (!c || (B && (!in || !trlwe_out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = h2d(c, c->s_a, in, B * w * 4);
+    const uint32_t *tv = nullptr;
+    if (!rc && testvec) {
+        rc = h2d(c, c->s_tv, testvec, 2 * c->P.N * 4);
+        tv = (const uint32_t *)c->s_tv.p;
+    }
+    if (!rc) rc = ensure(c, c->s_out, B * 2 * c->P.N * 4);
+    if (!rc) rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, tv, (uint32_t *)c->s_out.p, B, false);
+    if (!rc) rc = d2h_sync(c, trlwe_out, c->s_out.p, B * 2 * c->P.N * 4);
+    return rc;
+}
+
+int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *out,
+                                 size_t B) {
+    if (!c || !testvec || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = h2d(c, c->s_a, in, B * w * 4);
+    if (!rc) rc = h2d(c, c->s_tv, testvec, 2 * c->P.N * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * w * 4);
+    if (!rc)
+        rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, (const uint32_t *)c->s_tv.p,
+                               (uint32_t *)c->s_out.p, B, true);
+    if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
+    return rc;
+}
+
+int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *c, const uint8_t *ops_dev, const uint32_t *a_dev, const uint32_t *b_dev,
+                            uint32_t *out_dev, size_t B) {
+    if (!c || (B && (!ops_dev || !a_dev || !b_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    return run_bootstrap_dev(c, ops_dev, a_dev, b_dev, nullptr, out_dev, B, true);
+}
+
+int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *c, const uint32_t *in_dev, uint32_t *out_dev, size_t B) {
+    if (!c || (B && (!in_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    return run_bootstrap_dev(c, nullptr, in_dev, nullptr, nullptr, out_dev, B, true);
+}
+
+int tfhe_gpu_fft_forward_batch(tfhe_gpu_ctx *c, const uint32_t *in, double *out, size_t B) {
+    if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = h2d(c, c->s_a, in, B * 1024 * 4);
+    if (!rc) rc = ensure(c, c->s_tmp, B * 1024 * 8);
+    if (rc) return rc;
+    HIPCHK(c, launch_fft_forward(tables(c), (const uint32_t *)c->s_a.p, (double *)c->s_tmp.p, B, c->stream));
+    return d2h_sync(c, out, c->s_tmp.p, B * 1024 * 8);
+}
+
+int tfhe_gpu_fft_inverse_batch(tfhe_gpu_ctx *c, const double *in, uint32_t *out, size_t B) {
+    if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = h2d(c, c->s_tmp, in, B * 1024 * 8);
+    if (!rc) rc = ensure(c, c->s_out, B * 1024 * 4);
+    if (rc) return rc;
+    HIPCHK(c, launch_fft_inverse(tables(c), (const double *)c->s_tmp.p, (uint32_t *)c->s_out.p, B, c->stream));
+    return d2h_sync(c, out, c->s_out.p, B * 1024 * 4);
+}
+
+int tfhe_gpu_poly_mul_batch(tfhe_gpu_ctx *c, const uint32_t *a, const uint32_t *b, uint32_t *out, size_t B) {
+    if (!c || (B && (!a || !b || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = h2d(c, c->s_a, a, B * 1024 * 4);
+    if (!rc) rc = h2d(c, c->s_b, b, B * 1024 * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * 1024 * 4);
+    if (rc) return rc;
+    HIPCHK(c, launch_poly_mul(tables(c), (const uint32_t *)c->s_a.p, (const uint32_t *)c->s_b.p, 1024,
+                              (uint32_t *)c->s_out.p, B, c->stream));
+    return d2h_sync(c, out, c->s_out.p, B * 1024 * 4);
+}
+
+int tfhe_gpu_external_product_batch(tfhe_gpu_ctx *c, const double *trgsw_fft, uint32_t bk_index,
+                                    const uint32_t *in, uint32_t *out, size_t B) {
+    if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t row_d = (size_t)2 * c->P.L * 2048;  // doubles per TRGSW
+    const double *row = nullptr;
+    int rc = TFHE_OK;
+    if (trgsw_fft) {
+        rc = h2d(c, c->s_tmp, trgsw_fft, row_d * 8);
+        if (!rc) rc = ensure(c, c->s_tv, row_d * 8);
+        if (rc) return rc;
+        HIPCHK(c, launch_bk_permute(c->K, (const double *)c->s_tmp.p, (double *)c->s_tv.p, 2 * c->P.L, c->stream));
+        row = (const double *)c->s_tv.p;
+        if (c->K.offset == 0) {  // no key loaded yet: use the parameter set's offset
+            uint32_t off = 0;
+            for (uint32_t l = 0; l < c->P.L; l++)
+                off += ((1u << c->P.bgbit) / 2) * (1u << (32 - (l + 1) * c->P.bgbit));
+            c->K.offset = off;
+        }
+    } else {
+        if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+        if (bk_index >= c->P.n) return fail(c, TFHE_ERR_INVALID, "bk_index >= n");
+        row = c->d_bk + (size_t)bk_index * row_d;
+    }
+    rc = h2d(c, c->s_a, in, B * 2048 * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * 2048 * 4);
+    if (rc) return rc;
+    HIPCHK(c, launch_external_product(c->K, tables(c), row, (const uint32_t *)c->s_a.p, (uint32_t *)c->s_out.p, B,
+                                      c->stream));
+    return d2h_sync(c, out, c->s_out.p, B * 2048 * 4);
+}
+
+int tfhe_gpu_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t *in_lv1, uint32_t *out_lv0, size_t B) {
+    if (!c || (B && (!in_lv1 || !out_lv0))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = h2d(c, c->s_lv1, in_lv1, B * 1025 * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * w * 4);
+    if (rc) return rc;
+    HIPCHK(c, launch_key_switch(c->K, (const uint32_t *)c->s_lv1.p, c->d_ksk, (uint32_t *)c->s_out.p, B, c->stream));
+    return d2h_sync(c, out_lv0, c->s_out.p, B * w * 4);
+}
+
+// ---- host-side TLWELv0 helpers ------------------------------------------
+int tfhe_encrypt_bool_batch(const tfhe_params *p, const uint32_t *key, const uint8_t *bits, uint64_t seed0,
+                            uint32_t *out, size_t B) {
+    if (!p || !key || (B && (!bits || !out))) return TFHE_ERR_INVALID;
+    for (size_t i = 0; i < B; i++)
+        tlwe_encrypt(p->n, bits[i] ? 0.125 : -0.125, p->alpha_lv0, key, seed0 + i, out + i * (p->n + 1));
+    return TFHE_OK;
+}
+
+int tfhe_decrypt_bool_batch(const tfhe_params *p, const uint32_t *key, const uint32_t *ct, uint8_t *bits, size_t B) {
+    if (!p || !key || (B && (!bits || !ct))) return TFHE_ERR_INVALID;
+    for (size_t i = 0; i < B; i++) bits[i] = (int32_t)tlwe_phase(p->n, ct + i * (p->n + 1), key) >= 0;
+    return TFHE_OK;
+}
+
+int tfhe_encrypt_lwe_message_batch(const tfhe_params *p, const uint32_t *key, const uint32_t *msgs, uint32_t m,
+                                   uint64_t seed0, uint32_t *out, size_t B) {
+    if (!p || !key || m == 0 || (B && (!msgs || !out))) return TFHE_ERR_INVALID;
+    const double scale = 1.0 / (2.0 * (double)m);
+    for (size_t i = 0; i < B; i++)
+        tlwe_encrypt(p->n, (double)(msgs[i] % m) * scale, p->alpha_lv0, key, seed0 + i, out + i * (p->n + 1));
+    return TFHE_OK;
+}
+
+int tfhe_decrypt_lwe_message_batch(const tfhe_params *p, const uint32_t *key, const uint32_t *ct, uint32_t m,
+                                   uint32_t *msgs, size_t B) {
+    if (!p || !key || m == 0 || (B && (!msgs || !ct))) return TFHE_ERR_INVALID;
+    const double scale = 1.0 / (2.0 * (double)m);
+    for (size_t i = 0; i < B; i++) {
+        double f = (double)tlwe_phase(p->n, ct + i * (p->n + 1), key) / 4294967296.0;
+        msgs[i] = (uint32_t)((uint64_t)(f / scale + 0.5) % m);
+    }
+    return TFHE_OK;
+}
+
+int tfhe_lut_generate(const tfhe_params *p, uint32_t m, const uint32_t *f_table, uint32_t *tv) {
+    if (!p || !f_table || !tv || m == 0 || m > p->N) return TFHE_ERR_INVALID;
+    const size_t N = p->N;
+    std::vector<uint32_t> raw(N, 0u);
+    const double scale = 1.0 / (2.0 * (double)m);
+    auto div_round = [](size_t a, size_t b) { return (a + b / 2) / b; };
+    for (uint32_t x = 0; x < m; x++) {
+        size_t s = div_round((size_t)x * N, m), e = div_round((size_t)(x + 1) * N, m);
+        uint32_t enc = host::f64_to_torus((double)(f_table[x] % m) * scale);
+        for (size_t i = s; i < e; i++) raw[i] = enc;
+    }
+    size_t off = div_round(N, 2 * (size_t)m);
+    for (size_t i = 0; i < N; i++) tv[N + i] = raw[(i + off) % N];
+    for (size_t i = N - off; i < N; i++) tv[N + i] = ~tv[N + i] + 1u;
+    for (size_t i = 0; i < N; i++) tv[i] = 0;
+    return TFHE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,61 @@
+// tfhe_internal.hpp — shared declarations between the C-ABI host layer
+// (tfhe_gpu.cpp) and the HIP kernels (tfhe_kernels.hip).  Not installed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace tfhe {
+
+struct C2 {
+    double x, y;
+};
+
+// Device-side parameter block passed by value to every kernel.
+struct KParams {
+    int n;          // lv0 dimension
+    int N;          // 1024
+    int L;          // gadget levels
+    int bgbit;      // log2 Bg
+    int basebit;    // key-switch base bits
+    int iks_t;      // key-switch levels
+    uint32_t offset;  // decomposition offset (key.zig:121-131)
+};
+
+// Output forms of the blind-rotation kernel.
+enum BrOut : int {
+    BR_OUT_LV1 = 0,    // sampleExtractIndex(acc, 0): TLWELv1, N+1 words per item
+    BR_OUT_TRLWE = 1,  // the accumulator itself: TRLWELv1, 2N words per item
+};
+
+// Device constant tables uploaded once per context (host_tables in tfhe_gpu.cpp).
+struct DevTables {
+    const C2 *twist;  // N/2 twisting factors exp(i*pi*k/N)        fft.zig:92-106
+    const C2 *tw;     // N/2-1 forward stage twiddles (recurrence)  fft.zig:590-616
+};
+
+// ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------
+hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
+                               const uint32_t *in_a, const uint32_t *in_b,
+                               const uint32_t *testvec, const double *bkd, uint32_t *out,
+                               int out_mode, size_t B, hipStream_t s);
+hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
+                             uint32_t *out, size_t B, hipStream_t s);
+hipError_t launch_fft_forward(const DevTables &T, const uint32_t *in, double *out, size_t B,
+                              hipStream_t s);
+hipError_t launch_fft_inverse(const DevTables &T, const double *in, uint32_t *out, size_t B,
+                              hipStream_t s);
+// b_stride: words between consecutive b polynomials (0 = one b for all items)
+hipError_t launch_poly_mul(const DevTables &T, const uint32_t *a, const uint32_t *b, size_t b_stride,
+                           uint32_t *out, size_t B, hipStream_t s);
+hipError_t launch_external_product(const KParams &P, const DevTables &T, const double *bkd_row,
+                                   const uint32_t *in, uint32_t *out, size_t B, hipStream_t s);
+// reference BK layout [n][2L][2][N] -> device layout [n][2L][8][64] x {a_re,a_im,b_re,b_im}
+hipError_t launch_bk_permute(const KParams &P, const double *bk_ref, double *bkd, size_t rows,
+                             hipStream_t s);
+hipError_t launch_bk_unpermute(const KParams &P, const double *bkd, double *bk_ref, size_t rows,
+                               hipStream_t s);
+
+}  // namespace tfhe

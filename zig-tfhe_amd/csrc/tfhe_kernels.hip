@@ -1,0 +1,676 @@
+// tfhe_kernels.hip — CDNA4 (gfx950) kernels of the TFHE gate-bootstrap path.
+//
+// Hot path: trgsw.blindRotate (trgsw.zig:290-333) -> cmux (:260-284) ->
+// externalProductWithFft (:111-154) over the negacyclic f64 FFT
+// (fft.zig:293-443), then sampleExtractIndex (trlwe.zig:146-162) and
+// identityKeySwitching (trgsw.zig:471-502).
+//
+// Bit-exactness contract: every f64 operation of the
+// reference is performed with the same operands, the same expression tree and
+// round-to-nearest, no FMA contraction (file-wide `fp contract(off)` plus
+// -ffp-contract=off), twiddles uploaded from the host (never sin/cos on the
+// device).  Exact power-of-two rescalings (×2 in ifft1024, ×0.5 in
+// fmaInFd1024 and fft1024) are folded, which leaves every result bit-identical.
+//
+// FFT mapping: one wavefront owns one 512-point complex transform (N=1024
+// negacyclic), 8 complex values per lane, three radix-2^3 register passes
+// (each pass = three radix-2 DIT stages with the reference's butterflies and
+// recurrence twiddles) and two conflict-free LDS exchanges.
+// Lane t always owns coefficients / frequencies {t + 64q}, so the forward
+// output feeds the MAC and the inverse input with no data movement, and the
+// accumulator update is lane-local.
+#include <hip/hip_runtime.h>
+
+#include "tfhe_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace tfhe {
+
+#define DEV __device__ __forceinline__
+
+DEV C2 c2(double x, double y) {
+    C2 r;
+    r.x = x;
+    r.y = y;
+    return r;
+}
+
+// Complex.mul (fft.zig:50-55) by a forward twiddle; INV: by the inverse
+// table, which is the exact conjugate of the forward one (checked on the host
+// at table upload), written as the identical IEEE expression tree.
+template <bool INV>
+DEV C2 twmul(C2 a, C2 w) {
+    if (!INV) return c2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+    return c2(a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y);
+}
+
+// radix2FFT inner butterfly (fft.zig:600-606)
+template <bool INV>
+DEV void bf(C2 &u, C2 &x, C2 w) {
+    C2 v = twmul<INV>(x, w);
+    C2 a = c2(u.x + v.x, u.y + v.y);
+    C2 b = c2(u.x - v.x, u.y - v.y);
+    u = a;
+    x = b;
+}
+// j == 0 butterfly: the recurrence twiddle is exactly (1, 0); x*(1,0) == x up
+// to the sign of zero, which never reaches an output integer.
+DEV void bf1(C2 &u, C2 &x) {
+    C2 a = c2(u.x + x.x, u.y + x.y);
+    C2 b = c2(u.x - x.x, u.y - x.y);
+    u = a;
+    x = b;
+}
+
+DEV int br3(int q) { return ((q & 1) << 2) | (q & 2) | ((q >> 2) & 1); }
+DEV int br6(int t) { return (int)(__builtin_bitreverse32((uint32_t)t) >> 26); }
+
+// Per-lane twiddles.  Table index of stage len, j: len/2 - 1 + j.
+struct LaneTw {
+    C2 w4, w8_1, w8_2, w8_3;       // pass A (lane-uniform)
+    C2 w16, w32[2], w64[4];        // pass B, j = (t&7) + 8*...
+    C2 w128, w256[2], w512[4];     // pass C, j = t + 64*...
+};
+
+DEV void load_lane_tw(LaneTw &T, const C2 *__restrict__ tw, int t) {
+    T.w4 = tw[2];
+    T.w8_1 = tw[4];
+    T.w8_2 = tw[5];
+    T.w8_3 = tw[6];
+    int r = t & 7;
+    T.w16 = tw[7 + r];
+    T.w32[0] = tw[15 + r];
+    T.w32[1] = tw[15 + r + 8];
+#pragma unroll
+    for (int q = 0; q < 4; q++) T.w64[q] = tw[31 + r + 8 * q];
+    T.w128 = tw[63 + t];
+    T.w256[0] = tw[127 + t];
+    T.w256[1] = tw[127 + t + 64];
+#pragma unroll
+    for (int q = 0; q < 4; q++) T.w512[q] = tw[255 + t + 64 * q];
+}
+
+// Pass A: stages len = 2, 4, 8 (bits 0-2 of the bit-reversed position are the
+// register index q).
+template <bool INV>
+DEV void passA(C2 *d, const LaneTw &T) {
+    bf1(d[0], d[1]); bf1(d[2], d[3]); bf1(d[4], d[5]); bf1(d[6], d[7]);
+    bf1(d[0], d[2]); bf<INV>(d[1], d[3], T.w4); bf1(d[4], d[6]); bf<INV>(d[5], d[7], T.w4);
+    bf1(d[0], d[4]); bf<INV>(d[1], d[5], T.w8_1); bf<INV>(d[2], d[6], T.w8_2); bf<INV>(d[3], d[7], T.w8_3);
+}
+// Pass B: stages 16, 32, 64 (position bits 3-5 in q; j = (t&7) + 8*(...)).
+template <bool INV>
+DEV void passB(C2 *d, const LaneTw &T) {
+    bf<INV>(d[0], d[1], T.w16); bf<INV>(d[2], d[3], T.w16); bf<INV>(d[4], d[5], T.w16); bf<INV>(d[6], d[7], T.w16);
+    bf<INV>(d[0], d[2], T.w32[0]); bf<INV>(d[1], d[3], T.w32[1]); bf<INV>(d[4], d[6], T.w32[0]); bf<INV>(d[5], d[7], T.w32[1]);
+    bf<INV>(d[0], d[4], T.w64[0]); bf<INV>(d[1], d[5], T.w64[1]); bf<INV>(d[2], d[6], T.w64[2]); bf<INV>(d[3], d[7], T.w64[3]);
+}
+// Pass C: stages 128, 256, 512 (position bits 6-8 in q; j = t + 64*(...)).
+template <bool INV>
+DEV void passC(C2 *d, const LaneTw &T) {
+    bf<INV>(d[0], d[1], T.w128); bf<INV>(d[2], d[3], T.w128); bf<INV>(d[4], d[5], T.w128); bf<INV>(d[6], d[7], T.w128);
+    bf<INV>(d[0], d[2], T.w256[0]); bf<INV>(d[1], d[3], T.w256[1]); bf<INV>(d[4], d[6], T.w256[0]); bf<INV>(d[5], d[7], T.w256[1]);
+    bf<INV>(d[0], d[4], T.w512[0]); bf<INV>(d[1], d[5], T.w512[1]); bf<INV>(d[2], d[6], T.w512[2]); bf<INV>(d[3], d[7], T.w512[3]);
+}
+
+// Exchange 1 (after pass A): lane t wrote positions 8*br6(t)+q, reads
+// (t&7) + 8q + 64(t>>3).  XOR swizzle of the 16-B slot makes both the
+// ds_write_b128 and the ds_read_b128 bank-conflict-free.
+DEV int swz1(int p) {
+    return p ^ ((((p >> 6) & 1) * 1) ^ (((p >> 7) & 1) * 10) ^ (((p >> 8) & 1) * 4));
+}
+
+template <int NF>
+DEV void exchange1(C2 (*d)[8], C2 *xb, int t) {
+    int wb = 8 * br6(t);
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) xb[f * 512 + swz1(wb + q)] = d[f][q];
+    __syncthreads();
+    int rb = (t & 7) + 64 * (t >> 3);
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) d[f][q] = xb[f * 512 + swz1(rb + 8 * q)];
+    __syncthreads();
+}
+
+template <int NF>
+DEV void exchange2(C2 (*d)[8], C2 *xb, int t) {
+    int wb = (t & 7) + 64 * (t >> 3);
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) xb[f * 512 + wb + 8 * q] = d[f][q];
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < NF; f++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) d[f][q] = xb[f * 512 + t + 64 * q];
+    __syncthreads();
+}
+
+// 512-point radix-2 DIT (bitReverseRadix2 + radix2FFT, fft.zig:582-669) on NF
+// transforms at once.  In: d[f][q] = z[t + 64*br3(q)] (the bit reversal is
+// absorbed into the load order).  Out: d[f][q] = Z[t + 64q].
+template <int NF, bool INV>
+DEV void fft512(C2 (*d)[8], C2 *xb, const LaneTw &T, int t) {
+#pragma unroll
+    for (int f = 0; f < NF; f++) passA<INV>(d[f], T);
+    exchange1<NF>(d, xb, t);
+#pragma unroll
+    for (int f = 0; f < NF; f++) passB<INV>(d[f], T);
+    exchange2<NF>(d, xb, t);
+#pragma unroll
+    for (int f = 0; f < NF; f++) passC<INV>(d[f], T);
+}
+
+// Fold + twist of ifft1024 (fft.zig:301-323): z = (x_re, x_im) * twist.
+DEV C2 twist_in(double xr, double xi, C2 w) { return c2(xr * w.x - xi * w.y, xr * w.y + xi * w.x); }
+
+// Untwist + normalisation of fft1024 (fft.zig:412-429).  `f` is 2x the
+// reference's value (the ×0.5 input scaling is folded), hence 1/(2*512).
+DEV void untwist_out(C2 f, C2 w, double &tr, double &ti) {
+    const double norm = 1.0 / 1024.0;
+    tr = (f.x * w.x + f.y * w.y) * norm;
+    ti = (f.y * w.x - f.x * w.y) * norm;
+}
+
+// @round (half away from zero) -> i64 -> @truncate i32 -> u32 == r mod 2^32,
+// computed exactly in f64 for any finite r.
+DEV uint32_t torus_from_f64(double v) {
+    double r = round(v);
+    double hi = floor(r * (1.0 / 4294967296.0));
+    double lo = r - hi * 4294967296.0;
+    return (uint32_t)lo;
+}
+
+// decompositionIntoStorage digit (trgsw.zig:207-217); `x` already has the
+// decomposition offset added.
+DEV double digit_f64(uint32_t x, int level, int bgbit) {
+    uint32_t d = ((x >> (32 - (level + 1) * bgbit)) & ((1u << bgbit) - 1u)) - (1u << (bgbit - 1));
+    return (double)(int32_t)d;
+}
+
+// X^k rotation read (polyMulWithXK, trgsw.zig:442-466) of coefficient k from
+// the accumulator polynomial `p` (N=1024) held in LDS, k in [0, 2N].
+DEV uint32_t rot_read(const uint32_t *p, int k, int at) {
+    int idx = (k - at) & 2047;
+    uint32_t v = p[idx & 1023];
+    return (idx & 1024) ? 0u - v : v;
+}
+
+// Gate pre-combination, gates.zig:48-121 (constants utils.f64ToTorus).
+DEV uint32_t gate_combine(int op, uint32_t x, uint32_t y, bool is_b) {
+    uint32_t r;
+    switch (op) {
+    case 0: r = (0u - x) + (0u - y); break;              // NAND
+    case 1: case 2: r = x + y; break;                    // OR, AND
+    case 3: r = x + y * 2u; break;                       // XOR  (addMul)
+    case 4: r = x - y * 2u; break;                       // XNOR (subMul)
+    case 5: r = (0u - x) + (0u - y); break;              // NOR
+    case 6: case 8: r = (0u - x) + y; break;             // ANDNY, ORNY
+    case 7: case 9: r = x - y; break;                    // ANDYN, ORYN
+    default: return x;                                   // COPY
+    }
+    if (is_b) {
+        switch (op) {
+        case 0: case 1: case 8: case 9: r += 0x20000000u; break;  // +f64ToTorus(0.125)
+        case 2: case 5: case 6: case 7: r += 0xE0000000u; break;  // +f64ToTorus(-0.125)
+        case 3: r += 0x40000000u; break;                          // +f64ToTorus(0.25)
+        case 4: r += 0xC0000000u; break;                          // +f64ToTorus(-0.25)
+        default: break;
+        }
+    }
+    return r;
+}
+
+// Load an fft512 input pair from the decomposed accumulator difference.
+// src[m] holds (rot - acc + offset) at coefficient t + 64m, m < 16.
+// `row` may be a runtime value: the a/b source is chosen per element by a
+// select, never by indexing a register array dynamically (no scratch).
+template <int L>
+DEV void load_digits(C2 *d, const uint32_t *srcA, const uint32_t *srcB, int row, int bgbit,
+                     const C2 *twl) {
+    const bool from_a = row < L;
+    const int level = from_a ? row : row - L;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        int m = br3(q);
+        uint32_t re = from_a ? srcA[m] : srcB[m];
+        uint32_t im = from_a ? srcA[m + 8] : srcB[m + 8];
+        d[q] = twist_in(digit_f64(re, level, bgbit), digit_f64(im, level, bgbit), twl[m]);
+    }
+}
+
+// One frequency-domain multiply-accumulate row (fmaInFd1024, trgsw.zig:157-189)
+// for both output polynomials; bk = {a_re, a_im, b_re, b_im} at frequency
+// t + 64q.  `first`: the reference starts from 0.0, and 0.0 + x == x.
+DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double4 *__restrict__ bk, int t, bool first) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        double4 k = bk[q * 64 + t];
+        C2 ta = c2(d[q].x * k.x - d[q].y * k.y, d[q].x * k.y + d[q].y * k.x);
+        C2 tb = c2(d[q].x * k.z - d[q].y * k.w, d[q].x * k.w + d[q].y * k.z);
+        if (first) {
+            fa[q] = ta;
+            fb[q] = tb;
+        } else {
+            fa[q] = c2(fa[q].x + ta.x, fa[q].y + ta.y);
+            fb[q] = c2(fb[q].x + tb.x, fb[q].y + tb.y);
+        }
+    }
+}
+
+// ExternalProduct(BK row, tmp) for one TRLWE, tmp given per lane as
+// (value + offset) at coefficients t + 64m; returns the torus result added to
+// `accA/accB` (cmux: acc' = ExtProd + acc).
+template <int L>
+DEV void external_product_add(const uint32_t *tA, const uint32_t *tB, const double4 *__restrict__ bkrow,
+                              int bgbit, const LaneTw &T, const C2 *twl, C2 *xb, int t,
+                              uint32_t *accA, uint32_t *accB) {
+    C2 fa[8], fb[8];
+#pragma unroll 1
+    for (int rp = 0; rp < L; rp++) {
+        C2 d[2][8];
+        load_digits<L>(d[0], tA, tB, 2 * rp, bgbit, twl);
+        load_digits<L>(d[1], tA, tB, 2 * rp + 1, bgbit, twl);
+        fft512<2, false>(d, xb, T, t);
+        mac_row(fa, fb, d[0], bkrow + (size_t)(2 * rp) * 512, t, rp == 0);
+        mac_row(fa, fb, d[1], bkrow + (size_t)(2 * rp + 1) * 512, t, false);
+    }
+    C2 e[2][8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        e[0][q] = fa[br3(q)];
+        e[1][q] = fb[br3(q)];
+    }
+    fft512<2, true>(e, xb, T, t);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        double ra, ia, rb, ib;
+        untwist_out(e[0][q], twl[q], ra, ia);
+        untwist_out(e[1][q], twl[q], rb, ib);
+        accA[q] += torus_from_f64(ra);
+        accA[q + 8] += torus_from_f64(ia);
+        accB[q] += torus_from_f64(rb);
+        accB[q + 8] += torus_from_f64(ib);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Blind rotation, one wavefront per item, all n CMUX steps in one launch.
+//   acc = X^{b~} * testvec;  for i < n: acc = CMUX(BK[i], acc, X^{a~_i} acc)
+// then either sampleExtractIndex(acc, 0) (TLWELv1) or the TRLWE itself.
+// ---------------------------------------------------------------------------
+template <int L>
+__global__ __launch_bounds__(64, 1) void k_blind_rotate(
+    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ testvec,
+    const double4 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode) {
+    __shared__ uint32_t s_acc[2048];
+    __shared__ C2 s_x[2 * 512];
+    __shared__ uint16_t s_at[1024];
+    __shared__ int s_bt;
+
+    const int t = threadIdx.x;
+    const size_t g = blockIdx.x;
+    const int n = P.n;
+    const uint32_t *A = in_a + g * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + g * (size_t)(n + 1) : A;
+    const int op = ops ? (int)ops[g] : 255;
+
+    // a~_i = (a_i + 2^20) >> 21 and b~ = 2N - ((b + 2^20) >> 21), 64-bit adds
+    // (trgsw.zig:297, :312).
+    for (int i = t; i <= n; i += 64) {
+        uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
+        uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
+        if (i < n) s_at[i] = (uint16_t)tl;
+        else s_bt = 2048 - (int)tl;
+    }
+    LaneTw T;
+    load_lane_tw(T, TT.tw, t);
+    C2 twl[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) twl[m] = TT.twist[t + 64 * m];
+    __syncthreads();
+
+    // acc = X^{b~} * testvec (trgsw.zig:300-306), lane owns k = t + 64m.
+    uint32_t accA[16], accB[16];
+    const int bt = s_bt;
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        accA[m] = rot_read(testvec, t + 64 * m, bt);
+        accB[m] = rot_read(testvec + 1024, t + 64 * m, bt);
+        s_acc[t + 64 * m] = accA[m];
+        s_acc[1024 + t + 64 * m] = accB[m];
+    }
+    __syncthreads();
+
+    const size_t row_stride = (size_t)2 * L * 512;  // double4 per BK row (TRGSW)
+    for (int i = 0; i < n; i++) {
+        const int at = s_at[i];
+        // a~ in {0, 2N}: rot == acc, tmp == 0, every digit is 0 and the
+        // external product is exactly 0 -> the step is an exact no-op.
+        if (at == 0 || at == 2048) continue;
+        uint32_t tA[16], tB[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            tA[m] = rot_read(s_acc, t + 64 * m, at) - accA[m] + P.offset;
+            tB[m] = rot_read(s_acc + 1024, t + 64 * m, at) - accB[m] + P.offset;
+        }
+        external_product_add<L>(tA, tB, bkd + (size_t)i * row_stride, P.bgbit, T, twl, s_x, t, accA,
+                                accB);
+        __syncthreads();  // all lanes done reading the old accumulator
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            s_acc[t + 64 * m] = accA[m];
+            s_acc[1024 + t + 64 * m] = accB[m];
+        }
+        __syncthreads();
+    }
+
+    if (out_mode == BR_OUT_LV1) {
+        // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
+        uint32_t *o = out + g * (size_t)1025;
+        for (int j = t; j <= 1024; j += 64) {
+            uint32_t v;
+            if (j == 0) v = s_acc[0];
+            else if (j < 1024) v = 0u - s_acc[1024 - j];
+            else v = s_acc[1024];
+            o[j] = v;
+        }
+    } else {
+        uint32_t *o = out + g * (size_t)2048;
+        for (int j = t; j < 2048; j += 64) o[j] = s_acc[j];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Identity key switching (trgsw.zig:471-502).  Block = 256 output words x G
+// items; per (i, j) every item picks row k of the 2^basebit candidates; the
+// candidates are shared by the G items through L1.
+// ---------------------------------------------------------------------------
+template <int G>
+__global__ __launch_bounds__(256) void k_key_switch(KParams P, const uint32_t *__restrict__ lv1,
+                                                    const uint32_t *__restrict__ ksk,
+                                                    uint32_t *__restrict__ out, size_t B) {
+    __shared__ uint32_t s_in[G][1025];
+    const size_t g0 = (size_t)blockIdx.y * G;
+    const int w = blockIdx.x * 256 + threadIdx.x;
+    const int n1 = P.n + 1;
+    for (int x = threadIdx.x; x < G * 1025; x += 256) {
+        int gi = x / 1025, e = x % 1025;
+        s_in[gi][e] = (g0 + gi < B) ? lv1[(g0 + gi) * 1025 + e] : 0u;
+    }
+    __syncthreads();
+    uint32_t res[G];
+#pragma unroll
+    for (int gi = 0; gi < G; gi++) res[gi] = (w == P.n) ? s_in[gi][1024] : 0u;
+    const int basebit = P.basebit, T = P.iks_t, base = 1 << basebit;
+    const uint32_t prec = 1u << (32 - (1 + basebit * T));
+    const bool active = w < n1;
+    for (int i = 0; i < 1024; i++) {
+        const uint32_t *rows_i = ksk + (size_t)base * T * i * n1;
+        for (int j = 0; j < T; j++) {
+            const int sh = 32 - (j + 1) * basebit;
+#pragma unroll
+            for (int gi = 0; gi < G; gi++) {
+                uint32_t k = ((s_in[gi][i] + prec) >> sh) & (uint32_t)(base - 1);
+                if (k != 0 && active) res[gi] -= rows_i[((size_t)base * j + k) * n1 + w];
+            }
+        }
+    }
+    if (active) {
+#pragma unroll
+        for (int gi = 0; gi < G; gi++)
+            if (g0 + gi < B) out[(g0 + gi) * n1 + w] = res[gi];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stage kernels (parity tests and key generation); same device FFT.
+// ---------------------------------------------------------------------------
+// ifft1024: u32 -> f64 [re(512) | im(512)], ×2 (fft.zig:293-366)
+__global__ __launch_bounds__(64) void k_fft_forward(DevTables TT, const uint32_t *__restrict__ in,
+                                                    double *__restrict__ out) {
+    __shared__ C2 s_x[512];
+    const int t = threadIdx.x;
+    const uint32_t *x = in + (size_t)blockIdx.x * 1024;
+    LaneTw T;
+    load_lane_tw(T, TT.tw, t);
+    C2 d[1][8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        int k = t + 64 * br3(q);
+        d[0][q] = twist_in((double)(int32_t)x[k], (double)(int32_t)x[k + 512], TT.twist[k]);
+    }
+    fft512<1, false>(d, s_x, T, t);
+    double *o = out + (size_t)blockIdx.x * 1024;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        o[t + 64 * q] = d[0][q].x * 2.0;
+        o[512 + t + 64 * q] = d[0][q].y * 2.0;
+    }
+}
+
+// fft1024: f64 -> u32 (fft.zig:370-443).  Input ×0.5 folded into 1/1024.
+__global__ __launch_bounds__(64) void k_fft_inverse(DevTables TT, const double *__restrict__ in,
+                                                    uint32_t *__restrict__ out) {
+    __shared__ C2 s_x[512];
+    const int t = threadIdx.x;
+    const double *f = in + (size_t)blockIdx.x * 1024;
+    LaneTw T;
+    load_lane_tw(T, TT.tw, t);
+    C2 d[1][8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        int k = t + 64 * br3(q);
+        d[0][q] = c2(f[k], f[k + 512]);
+    }
+    fft512<1, true>(d, s_x, T, t);
+    uint32_t *o = out + (size_t)blockIdx.x * 1024;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        double tr, ti;
+        untwist_out(d[0][q], TT.twist[t + 64 * q], tr, ti);
+        o[t + 64 * q] = torus_from_f64(tr);
+        o[512 + t + 64 * q] = torus_from_f64(ti);
+    }
+}
+
+// poly_mul (fft.zig:458-492): ifft(a), ifft(b), (ar*br - ai*bi)*0.5, fft.
+// With the ×2 of both ifft outputs and the ×0.5s folded: P = A*B computed on
+// the unscaled transforms equals ref/2 exactly; fft's ×0.5 then cancels it.
+__global__ __launch_bounds__(64) void k_poly_mul(DevTables TT, const uint32_t *__restrict__ a,
+                                                 const uint32_t *__restrict__ b, size_t b_stride,
+                                                 uint32_t *__restrict__ out) {
+    __shared__ C2 s_x[2 * 512];
+    const int t = threadIdx.x;
+    const uint32_t *x = a + (size_t)blockIdx.x * 1024;
+    const uint32_t *y = b + (size_t)blockIdx.x * b_stride;
+    LaneTw T;
+    load_lane_tw(T, TT.tw, t);
+    C2 twl[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) twl[m] = TT.twist[t + 64 * m];
+    C2 d[2][8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        int m = br3(q), k = t + 64 * m;
+        d[0][q] = twist_in((double)(int32_t)x[k], (double)(int32_t)x[k + 512], twl[m]);
+        d[1][q] = twist_in((double)(int32_t)y[k], (double)(int32_t)y[k + 512], twl[m]);
+    }
+    fft512<2, false>(d, s_x, T, t);
+    // reference: r = (2A_r*2B_r - 2A_i*2B_i)*0.5 = 2*(A_r*B_r - A_i*B_i) exactly;
+    // fft then multiplies by 0.5, so the inverse input is P below, unscaled,
+    // and the final normalisation is 1/512 (not 1/1024).
+    C2 e[1][8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        C2 p = c2(d[0][q].x * d[1][q].x - d[0][q].y * d[1][q].y,
+                  d[0][q].x * d[1][q].y + d[0][q].y * d[1][q].x);
+        e[0][br3(q)] = p;
+    }
+    fft512<1, true>(e, s_x, T, t);
+    uint32_t *o = out + (size_t)blockIdx.x * 1024;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        C2 f = e[0][q], w = twl[q];
+        const double norm = 1.0 / 512.0;
+        double tr = (f.x * w.x + f.y * w.y) * norm;
+        double ti = (f.y * w.x - f.x * w.y) * norm;
+        o[t + 64 * q] = torus_from_f64(tr);
+        o[512 + t + 64 * q] = torus_from_f64(ti);
+    }
+}
+
+// externalProductWithFft (trgsw.zig:111-154) of B TRLWEs against one
+// device-layout TRGSW row.
+template <int L>
+__global__ __launch_bounds__(64) void k_external_product(KParams P, DevTables TT,
+                                                         const double4 *__restrict__ bkrow,
+                                                         const uint32_t *__restrict__ in,
+                                                         uint32_t *__restrict__ out) {
+    __shared__ C2 s_x[2 * 512];
+    const int t = threadIdx.x;
+    const uint32_t *x = in + (size_t)blockIdx.x * 2048;
+    LaneTw T;
+    load_lane_tw(T, TT.tw, t);
+    C2 twl[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) twl[m] = TT.twist[t + 64 * m];
+    uint32_t tA[16], tB[16], accA[16], accB[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        tA[m] = x[t + 64 * m] + P.offset;
+        tB[m] = x[1024 + t + 64 * m] + P.offset;
+        accA[m] = 0;
+        accB[m] = 0;
+    }
+    external_product_add<L>(tA, tB, bkrow, P.bgbit, T, twl, s_x, t, accA, accB);
+    uint32_t *o = out + (size_t)blockIdx.x * 2048;
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        o[t + 64 * m] = accA[m];
+        o[1024 + t + 64 * m] = accB[m];
+    }
+}
+
+// BK layout permutation: ref [rows][2][1024] (a|b, each re[512] ++ im[512])
+// <-> device [rows][8][64] double4 {a_re, a_im, b_re, b_im} at freq t + 64q.
+__global__ void k_bk_permute(const double *__restrict__ ref, double4 *__restrict__ dev, size_t rows,
+                             int dir) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= rows * 512) return;
+    size_t row = idx / 512;
+    int pos = (int)(idx % 512);
+    int q = pos >> 6, t = pos & 63;  // pos = t + 64q
+    const size_t rb = row * 2048;
+    double4 *dp = dev + row * 512 + (size_t)q * 64 + t;
+    if (dir == 0) {
+        double4 v;
+        v.x = ref[rb + pos];
+        v.y = ref[rb + 512 + pos];
+        v.z = ref[rb + 1024 + pos];
+        v.w = ref[rb + 1536 + pos];
+        *dp = v;
+    } else {
+        double4 v = *dp;
+        double *r = const_cast<double *>(ref);
+        r[rb + pos] = v.x;
+        r[rb + 512 + pos] = v.y;
+        r[rb + 1024 + pos] = v.z;
+        r[rb + 1536 + pos] = v.w;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
+                               const uint32_t *in_a, const uint32_t *in_b, const uint32_t *testvec,
+                               const double *bkd, uint32_t *out, int out_mode, size_t B,
+                               hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    dim3 grid((unsigned)B), block(64);
+    const double4 *bk4 = reinterpret_cast<const double4 *>(bkd);
+    switch (P.L) {
+    case 1:
+        hipLaunchKernelGGL(k_blind_rotate<1>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk4, out,
+                           out_mode);
+        break;
+    case 2:
+        hipLaunchKernelGGL(k_blind_rotate<2>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk4, out,
+                           out_mode);
+        break;
+    case 3:
+        hipLaunchKernelGGL(k_blind_rotate<3>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk4, out,
+                           out_mode);
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk, uint32_t *out,
+                             size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    constexpr int G = 8;
+    dim3 grid((unsigned)((P.n + 1 + 255) / 256), (unsigned)((B + G - 1) / G)), block(256);
+    hipLaunchKernelGGL(k_key_switch<G>, grid, block, 0, s, P, lv1, ksk, out, B);
+    return hipGetLastError();
+}
+
+hipError_t launch_fft_forward(const DevTables &T, const uint32_t *in, double *out, size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fft_forward, dim3((unsigned)B), dim3(64), 0, s, T, in, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fft_inverse(const DevTables &T, const double *in, uint32_t *out, size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fft_inverse, dim3((unsigned)B), dim3(64), 0, s, T, in, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_poly_mul(const DevTables &T, const uint32_t *a, const uint32_t *b, size_t b_stride,
+                           uint32_t *out, size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_poly_mul, dim3((unsigned)B), dim3(64), 0, s, T, a, b, b_stride, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_external_product(const KParams &P, const DevTables &T, const double *bkd_row,
+                                   const uint32_t *in, uint32_t *out, size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    const double4 *bk4 = reinterpret_cast<const double4 *>(bkd_row);
+    switch (P.L) {
+    case 1: hipLaunchKernelGGL(k_external_product<1>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk4, in, out); break;
+    case 2: hipLaunchKernelGGL(k_external_product<2>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk4, in, out); break;
+    case 3: hipLaunchKernelGGL(k_external_product<3>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk4, in, out); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_bk_permute(const KParams &, const double *bk_ref, double *bkd, size_t rows, hipStream_t s) {
+    size_t total = rows * 512;
+    if (!total) return hipSuccess;
+    hipLaunchKernelGGL(k_bk_permute, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, bk_ref,
+                       reinterpret_cast<double4 *>(bkd), rows, 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_bk_unpermute(const KParams &, const double *bkd, double *bk_ref, size_t rows, hipStream_t s) {
+    size_t total = rows * 512;
+    if (!total) return hipSuccess;
+    hipLaunchKernelGGL(k_bk_permute, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, bk_ref,
+                       reinterpret_cast<double4 *>(const_cast<double *>(bkd)), rows, 1);
+    return hipGetLastError();
+}
+
+}  // namespace tfhe

@@ -1,0 +1,411 @@
+"""Host-side mirror of zig-tfhe's public surface over the MI355X C ABI.
+
+Names follow the reference (src/gates.zig `Gates.nandGate` ..., src/key.zig
+`SecretKey` / `CloudKey`, src/tlwe.zig `TLWELv0`, src/params.zig parameter
+sets); every method is a thin call into lib/libtfhe_gpu.so (include/tfhe_gpu.h).
+There is no CPU fallback: without the built HIP library every entry point
+raises.
+
+Batches of ciphertexts are numpy uint32 arrays of shape (B, n+1) — B
+TLWELv0 values laid out exactly as `TLWELv0.p` (tlwe.zig:11-12).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libtfhe_gpu.so")
+
+# gate op codes, include/tfhe_gpu.h TFHE_GATE_* (gates.zig:48-121)
+NAND, OR, AND, XOR, XNOR, NOR, ANDNY, ANDYN, ORNY, ORYN = range(10)
+COPY = 255
+GATE_NAMES = {"nand": NAND, "or": OR, "and": AND, "xor": XOR, "xnor": XNOR, "nor": NOR,
+              "andny": ANDNY, "andyn": ANDYN, "orny": ORNY, "oryn": ORYN}
+
+
+class TfheParams(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("N", C.c_uint32), ("nbit", C.c_uint32), ("L", C.c_uint32),
+                ("bgbit", C.c_uint32), ("basebit", C.c_uint32), ("iks_t", C.c_uint32),
+                ("_pad", C.c_uint32), ("alpha_lv0", C.c_double), ("alpha_lv1", C.c_double),
+                ("alpha_ksk", C.c_double), ("alpha_bsk", C.c_double)]
+
+    def __repr__(self):
+        return (f"TfheParams(n={self.n}, N={self.N}, L={self.L}, bgbit={self.bgbit}, "
+                f"basebit={self.basebit}, iks_t={self.iks_t})")
+
+
+# params.zig parameter sets (runtime form).  KSK/BSK noise: the reference's
+# KSK_ALPHA/BSK_ALPHA (params.zig:419-422) are the 128-bit constants; UINT4
+# keeps its own set's alphas.
+SECURITY_128_BIT = dict(n=700, N=1024, nbit=10, L=3, bgbit=6, basebit=2, iks_t=9,
+                        alpha_lv0=2.0e-5, alpha_lv1=2.0e-8, alpha_ksk=2.0e-5, alpha_bsk=2.0e-8)
+SECURITY_80_BIT = dict(n=550, N=1024, nbit=10, L=3, bgbit=6, basebit=2, iks_t=7,
+                       alpha_lv0=5.0e-5, alpha_lv1=3.73e-8, alpha_ksk=2.0e-5, alpha_bsk=2.0e-8)
+SECURITY_UINT4 = dict(n=820, N=1024, nbit=10, L=1, bgbit=22, basebit=5, iks_t=3,
+                      alpha_lv0=0.00000251676160959795544987084234,
+                      alpha_lv1=0.00000000000000022204460492503131,
+                      alpha_ksk=0.00000251676160959795544987084234,
+                      alpha_bsk=0.00000000000000022204460492503131)
+PARAM_SETS = {"128": SECURITY_128_BIT, "80": SECURITY_80_BIT, "uint4": SECURITY_UINT4}
+
+
+def make_params(name_or_dict="128") -> TfheParams:
+    d = PARAM_SETS[name_or_dict] if isinstance(name_or_dict, str) else name_or_dict
+    return TfheParams(**d)
+
+
+_lib = None
+u32p, f64p, u8p, vp = C.POINTER(C.c_uint32), C.POINTER(C.c_double), C.POINTER(C.c_uint8), C.c_void_p
+
+_SIGS = {
+    "tfhe_gpu_abi_version": (C.c_int, []),
+    "tfhe_gpu_create": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(vp)]),
+    "tfhe_gpu_destroy": (None, [vp]),
+    "tfhe_gpu_last_error": (C.c_char_p, [vp]),
+    "tfhe_gpu_sync": (C.c_int, [vp]),
+    "tfhe_gpu_set_stream": (C.c_int, [vp, vp]),
+    "tfhe_gpu_load_cloud_key": (C.c_int, [vp, C.c_uint32, u32p, u32p, f64p, C.c_size_t, u32p, C.c_size_t]),
+    "tfhe_gpu_keygen": (C.c_int, [vp, C.c_uint64, C.c_uint64, u32p, u32p, f64p, u32p]),
+    "tfhe_gpu_key_blob_bytes": (C.c_int, [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "tfhe_gpu_export_key_device": (C.c_int, [vp, vp, vp, u32p, u32p]),
+    "tfhe_gpu_import_key_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p]),
+    "tfhe_gpu_bootstrap_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_gate_batch": (C.c_int, [vp, u8p, u32p, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_blind_rotate_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_bootstrap_lut_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_gate_batch_dev": (C.c_int, [vp, vp, vp, vp, vp, C.c_size_t]),
+    "tfhe_gpu_bootstrap_batch_dev": (C.c_int, [vp, vp, vp, C.c_size_t]),
+    "tfhe_gpu_fft_forward_batch": (C.c_int, [vp, u32p, f64p, C.c_size_t]),
+    "tfhe_gpu_fft_inverse_batch": (C.c_int, [vp, f64p, u32p, C.c_size_t]),
+    "tfhe_gpu_poly_mul_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_external_product_batch": (C.c_int, [vp, f64p, C.c_uint32, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_key_switch_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
+    "tfhe_encrypt_bool_batch": (C.c_int, [C.POINTER(TfheParams), u32p, u8p, C.c_uint64, u32p, C.c_size_t]),
+    "tfhe_decrypt_bool_batch": (C.c_int, [C.POINTER(TfheParams), u32p, u32p, u8p, C.c_size_t]),
+    "tfhe_encrypt_lwe_message_batch": (C.c_int, [C.POINTER(TfheParams), u32p, u32p, C.c_uint32, C.c_uint64,
+                                                 u32p, C.c_size_t]),
+    "tfhe_decrypt_lwe_message_batch": (C.c_int, [C.POINTER(TfheParams), u32p, u32p, C.c_uint32, u32p,
+                                                 C.c_size_t]),
+    "tfhe_lut_generate": (C.c_int, [C.POINTER(TfheParams), C.c_uint32, u32p, u32p]),
+}
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load the HIP library; raises (no fallback) if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libtfhe_gpu.so not built ({path}); run __graft_entry__.build() "
+                           "or `make -C zig-tfhe_amd`")
+    # If PyTorch is present, load its HIP runtime first: its libamdhip64 has
+    # the same SONAME, so this library then binds to it and device pointers /
+    # streams from torch are valid here (one runtime per process).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _u32(a):
+    a = np.ascontiguousarray(a, dtype=np.uint32)
+    return a, a.ctypes.data_as(u32p)
+
+
+def _f64(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(f64p)
+
+
+class TfheError(RuntimeError):
+    pass
+
+
+class Context:
+    """One HIP device + its resident CloudKey (tfhe_gpu_ctx)."""
+
+    def __init__(self, params="128", device: int = 0):
+        self.lib = load_library()
+        self.params = make_params(params) if not isinstance(params, TfheParams) else params
+        h = vp()
+        rc = self.lib.tfhe_gpu_create(C.byref(self.params), device, C.byref(h))
+        if rc != 0:
+            raise TfheError(f"tfhe_gpu_create failed ({rc})")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tfhe_gpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int, what: str):
+        if rc != 0:
+            raise TfheError(f"{what}: status {rc}: {self.lib.tfhe_gpu_last_error(self.h).decode()}")
+
+    @property
+    def n1(self) -> int:
+        return self.params.n + 1
+
+    # ---- keys
+    def load_cloud_key(self, offset, testvec, bk, ksk):
+        tv, _ = _u32(testvec)
+        bk, bkp = _f64(bk)
+        ksk, kp = _u32(ksk)
+        N = self.params.N
+        self.check(self.lib.tfhe_gpu_load_cloud_key(self.h, offset, tv[:N].ctypes.data_as(u32p),
+                                                    tv[N:].ctypes.data_as(u32p), bkp, bk.size, kp, ksk.size),
+                   "load_cloud_key")
+
+    def keygen(self, secret_seed: int, cloud_seed: int, want_host_copy: bool = False):
+        p = self.params
+        k0 = np.zeros(p.n, np.uint32)
+        k1 = np.zeros(p.N, np.uint32)
+        bk = ksk = None
+        bkp = kp = None
+        if want_host_copy:
+            bk = np.zeros((p.n, 2 * p.L, 2, p.N), np.float64)
+            ksk = np.zeros((p.N * p.iks_t * (1 << p.basebit), p.n + 1), np.uint32)
+            bkp, kp = bk.ctypes.data_as(f64p), ksk.ctypes.data_as(u32p)
+        self.check(self.lib.tfhe_gpu_keygen(self.h, secret_seed, cloud_seed, k0.ctypes.data_as(u32p),
+                                            k1.ctypes.data_as(u32p), bkp, kp), "keygen")
+        return SecretKey(p, k0, k1), (bk, ksk)
+
+    def key_blob_bytes(self):
+        a, b = C.c_size_t(), C.c_size_t()
+        self.check(self.lib.tfhe_gpu_key_blob_bytes(self.h, C.byref(a), C.byref(b)), "key_blob_bytes")
+        return a.value, b.value
+
+    def export_key_device(self, bk_dev_ptr: int, ksk_dev_ptr: int):
+        off = C.c_uint32()
+        tv = np.zeros(2 * self.params.N, np.uint32)
+        self.check(self.lib.tfhe_gpu_export_key_device(self.h, vp(bk_dev_ptr), vp(ksk_dev_ptr), C.byref(off),
+                                                       tv.ctypes.data_as(u32p)), "export_key_device")
+        return off.value, tv
+
+    def import_key_device(self, bk_dev_ptr: int, ksk_dev_ptr: int, offset: int, testvec):
+        tv, tvp = _u32(testvec)
+        self.check(self.lib.tfhe_gpu_import_key_device(self.h, vp(bk_dev_ptr), vp(ksk_dev_ptr), offset, tvp),
+                   "import_key_device")
+
+    def set_stream(self, stream_ptr: int | None):
+        self.check(self.lib.tfhe_gpu_set_stream(self.h, vp(stream_ptr or 0)), "set_stream")
+
+    def sync(self):
+        self.check(self.lib.tfhe_gpu_sync(self.h), "sync")
+
+    # ---- batch bootstrap API
+    def bootstrap_batch(self, cts):
+        cts, cp = _u32(cts)
+        out = np.zeros_like(cts)
+        self.check(self.lib.tfhe_gpu_bootstrap_batch(self.h, cp, out.ctypes.data_as(u32p), cts.shape[0]),
+                   "bootstrap_batch")
+        return out
+
+    def gate_batch(self, ops, a, b):
+        ops = np.ascontiguousarray(ops, dtype=np.uint8)
+        a, ap = _u32(a)
+        b, bp = _u32(b)
+        out = np.zeros_like(a)
+        self.check(self.lib.tfhe_gpu_gate_batch(self.h, ops.ctypes.data_as(u8p), ap, bp,
+                                                out.ctypes.data_as(u32p), ops.size), "gate_batch")
+        return out
+
+    def blind_rotate_batch(self, cts, testvec=None):
+        cts, cp = _u32(cts)
+        out = np.zeros((cts.shape[0], 2 * self.params.N), np.uint32)
+        tvp = None
+        if testvec is not None:
+            tv, tvp = _u32(testvec)
+        self.check(self.lib.tfhe_gpu_blind_rotate_batch(self.h, cp, tvp, out.ctypes.data_as(u32p),
+                                                        cts.shape[0]), "blind_rotate_batch")
+        return out
+
+    def bootstrap_lut_batch(self, cts, testvec):
+        cts, cp = _u32(cts)
+        tv, tvp = _u32(testvec)
+        out = np.zeros_like(cts)
+        self.check(self.lib.tfhe_gpu_bootstrap_lut_batch(self.h, cp, tvp, out.ctypes.data_as(u32p),
+                                                         cts.shape[0]), "bootstrap_lut_batch")
+        return out
+
+    def gate_batch_dev(self, ops_ptr, a_ptr, b_ptr, out_ptr, B):
+        self.check(self.lib.tfhe_gpu_gate_batch_dev(self.h, vp(ops_ptr), vp(a_ptr), vp(b_ptr), vp(out_ptr), B),
+                   "gate_batch_dev")
+
+    def bootstrap_batch_dev(self, in_ptr, out_ptr, B):
+        self.check(self.lib.tfhe_gpu_bootstrap_batch_dev(self.h, vp(in_ptr), vp(out_ptr), B), "bootstrap_batch_dev")
+
+    # ---- stage entry points
+    def fft_forward(self, polys):
+        x, xp = _u32(np.atleast_2d(polys))
+        out = np.zeros(x.shape, np.float64)
+        self.check(self.lib.tfhe_gpu_fft_forward_batch(self.h, xp, out.ctypes.data_as(f64p), x.shape[0]),
+                   "fft_forward")
+        return out
+
+    def fft_inverse(self, freqs):
+        f, fp = _f64(np.atleast_2d(freqs))
+        out = np.zeros(f.shape, np.uint32)
+        self.check(self.lib.tfhe_gpu_fft_inverse_batch(self.h, fp, out.ctypes.data_as(u32p), f.shape[0]),
+                   "fft_inverse")
+        return out
+
+    def poly_mul(self, a, b):
+        a, ap = _u32(np.atleast_2d(a))
+        b, bp = _u32(np.atleast_2d(b))
+        out = np.zeros(a.shape, np.uint32)
+        self.check(self.lib.tfhe_gpu_poly_mul_batch(self.h, ap, bp, out.ctypes.data_as(u32p), a.shape[0]),
+                   "poly_mul")
+        return out
+
+    def external_product(self, trlwes, trgsw_fft=None, bk_index=0):
+        x, xp = _u32(np.atleast_2d(trlwes))
+        out = np.zeros(x.shape, np.uint32)
+        tp = None
+        if trgsw_fft is not None:
+            tg, tp = _f64(trgsw_fft)
+        self.check(self.lib.tfhe_gpu_external_product_batch(self.h, tp, bk_index, xp, out.ctypes.data_as(u32p),
+                                                            x.shape[0]), "external_product")
+        return out
+
+    def key_switch(self, lv1):
+        x, xp = _u32(np.atleast_2d(lv1))
+        out = np.zeros((x.shape[0], self.n1), np.uint32)
+        self.check(self.lib.tfhe_gpu_key_switch_batch(self.h, xp, out.ctypes.data_as(u32p), x.shape[0]),
+                   "key_switch")
+        return out
+
+
+@dataclass
+class SecretKey:
+    """key.SecretKey (key.zig:34-58): binary lv0 / lv1 keys."""
+    params: TfheParams
+    key_lv0: np.ndarray
+    key_lv1: np.ndarray
+
+    def encrypt_bool(self, bits, seed0: int = 1):
+        """TLWELv0.encryptBool per bit, DefaultPrng(seed0 + i) in place of getUniqueSeed()."""
+        lib = load_library()
+        bits = np.ascontiguousarray(np.atleast_1d(bits), dtype=np.uint8)
+        out = np.zeros((bits.size, self.params.n + 1), np.uint32)
+        rc = lib.tfhe_encrypt_bool_batch(C.byref(self.params), _u32(self.key_lv0)[1], bits.ctypes.data_as(u8p),
+                                         seed0, out.ctypes.data_as(u32p), bits.size)
+        if rc:
+            raise TfheError(f"encrypt_bool: {rc}")
+        return out
+
+    def decrypt_bool(self, cts):
+        lib = load_library()
+        cts, cp = _u32(np.atleast_2d(cts))
+        out = np.zeros(cts.shape[0], np.uint8)
+        rc = lib.tfhe_decrypt_bool_batch(C.byref(self.params), _u32(self.key_lv0)[1], cp,
+                                         out.ctypes.data_as(u8p), cts.shape[0])
+        if rc:
+            raise TfheError(f"decrypt_bool: {rc}")
+        return out.astype(bool)
+
+    def encrypt_lwe_message(self, msgs, m: int, seed0: int = 1):
+        lib = load_library()
+        msgs, mp = _u32(np.atleast_1d(msgs))
+        out = np.zeros((msgs.size, self.params.n + 1), np.uint32)
+        rc = lib.tfhe_encrypt_lwe_message_batch(C.byref(self.params), _u32(self.key_lv0)[1], mp, m, seed0,
+                                                out.ctypes.data_as(u32p), msgs.size)
+        if rc:
+            raise TfheError(f"encrypt_lwe_message: {rc}")
+        return out
+
+    def decrypt_lwe_message(self, cts, m: int):
+        lib = load_library()
+        cts, cp = _u32(np.atleast_2d(cts))
+        out = np.zeros(cts.shape[0], np.uint32)
+        rc = lib.tfhe_decrypt_lwe_message_batch(C.byref(self.params), _u32(self.key_lv0)[1], cp, m,
+                                                out.ctypes.data_as(u32p), cts.shape[0])
+        if rc:
+            raise TfheError(f"decrypt_lwe_message: {rc}")
+        return out
+
+
+def lut_generate(params: TfheParams, m: int, f) -> np.ndarray:
+    """Generator.generateLookupTable (lut/generator.zig:85-135) for f: x -> f(x), x < m."""
+    lib = load_library()
+    table = np.array([f(x) for x in range(m)], dtype=np.uint32)
+    tv = np.zeros(2 * params.N, np.uint32)
+    rc = lib.tfhe_lut_generate(C.byref(params), m, table.ctypes.data_as(u32p), tv.ctypes.data_as(u32p))
+    if rc:
+        raise TfheError(f"lut_generate: {rc}")
+    return tv
+
+
+class Gates:
+    """gates.Gates (gates.zig:25-152) on the MI355X bootstrap strategy.
+
+    Each *_gate accepts single ciphertexts (n+1,) or batches (B, n+1); NOT /
+    COPY / CONSTANT need no bootstrap and stay on the host like the reference.
+    """
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def bootstrap_strategy(self) -> str:  # gates.zig:43-45
+        return "mi355x"
+
+    def _gate(self, op, a, b):
+        a = np.atleast_2d(np.asarray(a, np.uint32))
+        b = np.atleast_2d(np.asarray(b, np.uint32))
+        single = np.asarray(a).ndim == 2 and a.shape[0] == 1
+        out = self.ctx.gate_batch(np.full(a.shape[0], op, np.uint8), a, b)
+        return out[0] if single else out
+
+    def nand_gate(self, a, b): return self._gate(NAND, a, b)
+    def or_gate(self, a, b): return self._gate(OR, a, b)
+    def and_gate(self, a, b): return self._gate(AND, a, b)
+    def xor_gate(self, a, b): return self._gate(XOR, a, b)
+    def xnor_gate(self, a, b): return self._gate(XNOR, a, b)
+    def nor_gate(self, a, b): return self._gate(NOR, a, b)
+    def and_ny_gate(self, a, b): return self._gate(ANDNY, a, b)
+    def and_yn_gate(self, a, b): return self._gate(ANDYN, a, b)
+    def or_ny_gate(self, a, b): return self._gate(ORNY, a, b)
+    def or_yn_gate(self, a, b): return self._gate(ORYN, a, b)
+
+    def mux_naive(self, a, b, c):
+        """muxNaive (gates.zig:124-129): AND(a,b) || AND(NOT a, c), then OR — 2 levels."""
+        a = np.atleast_2d(np.asarray(a, np.uint32))
+        b = np.atleast_2d(np.asarray(b, np.uint32))
+        c = np.atleast_2d(np.asarray(c, np.uint32))
+        B = a.shape[0]
+        lvl1 = self.ctx.gate_batch(np.full(2 * B, AND, np.uint8), np.concatenate([a, self.not_gate(a)]),
+                                   np.concatenate([b, c]))
+        return self.ctx.gate_batch(np.full(B, OR, np.uint8), lvl1[:B], lvl1[B:])
+
+    @staticmethod
+    def not_gate(a):  # gates.zig:132-135 (TLWELv0.neg)
+        return (np.uint32(0) - np.asarray(a, np.uint32)).astype(np.uint32)
+
+    @staticmethod
+    def copy(a):  # gates.zig:138-141
+        return np.array(a, np.uint32, copy=True)
+
+    def constant(self, value: bool):  # gates.zig:144-151
+        res = np.zeros(self.ctx.n1, np.uint32)
+        mu = 0x20000000  # f64ToTorus(0.125)
+        res[-1] = mu if value else (1 - mu) & 0xFFFFFFFF
+        return res
