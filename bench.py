@@ -1,0 +1,183 @@
+"""Gate-bootstrap throughput on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch: B NAND gates (128-bit
+params) = linear pre-combination + blind rotation (700 CMUX) + sample extract
++ identity key switch, inputs already resident in HBM.  One process per GPU
+(torch.distributed.run); per-GPU batch fixed (weak scaling); the cloud key is
+generated on rank 0 and broadcast once over RCCL/xGMI; no collective on the
+data path.  Rank 0 prints one JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--params 128]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zig-tfhe_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (loads the HIP runtime before libtfhe_gpu.so)
+import torch.distributed as dist  # noqa: E402
+
+import tfhe_dist as tdist  # noqa: E402
+import tfhe_amd  # noqa: E402
+
+HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md chip table (spec)
+METRIC = "gate-bootstraps/sec (NAND, 128-bit params) at 1/2/4/8 MI355X; % HBM roofline"
+
+
+def algorithmic_bytes_per_gate(p) -> int:
+    """Streamed-key model: each gate consumes every BK row once
+    (n*2L*2*N f64) + its two input TLWELv0 + the TLWELv1 it writes."""
+    return p.n * 2 * p.L * 2 * p.N * 8 + 2 * (p.n + 1) * 4 + (p.N + 1) * 4
+
+
+def cpu_baseline(p, sk, bk, ksk, A, B, gpu_out, seconds: float):
+    """Oracle (C restatement of zig-tfhe's CPU path, -O3) on the host cores,
+    on a bounded sample of the same workload; also spot-checks GPU bits."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import CloudKeyArrays, Oracle, params
+    o = Oracle(fast=True)
+    op = params("128")
+    ck = CloudKeyArrays(0x82080000, np.concatenate([np.zeros(p.N, np.uint32),
+                                                    np.full(p.N, 0x20000000, np.uint32)]), ksk, bk)
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    # parity spot check of the first gates of the GPU batch
+    nchk = min(cores, A.shape[0])
+    want = o.gate_batch(op, np.zeros(nchk, np.uint8), A[:nchk], B[:nchk], ck, threads=cores)
+    spot_ok = bool(np.array_equal(want, gpu_out[:nchk]))
+    # single-thread rate on a few gates, then all cores for ~`seconds`
+    t0 = time.perf_counter()
+    o.gate_batch(op, np.zeros(2, np.uint8), A[:2], B[:2], ck, threads=1)
+    st_rate = 2 / (time.perf_counter() - t0)
+    done, t0 = 0, time.perf_counter()
+    i = 0
+    while time.perf_counter() - t0 < seconds:
+        idx = (np.arange(cores) + i) % A.shape[0]
+        o.gate_batch(op, np.zeros(cores, np.uint8), A[idx], B[idx], ck, threads=cores)
+        done += cores
+        i += cores
+    rate = done / (time.perf_counter() - t0)
+    return {"value": round(rate, 2), "unit": "gate-bootstraps/s", "cores": cores, "kind": "port",
+            "sample": (f"{done} NAND gate bootstraps (128-bit) of the same batch, {cores} threads x 1 gate each, "
+                       f"~{seconds:.0f}s; single-thread {st_rate:.2f} gates/s; oracle/tfhe_oracle.c -O3"),
+            "parity_spot_check": {"gates": nchk, "bit_exact": spot_ok}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024, help="NAND gates per GPU per step")
+    ap.add_argument("--params", default="128")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = tdist.env_rank_world()
+    if world > 1:
+        dist.init_process_group("nccl")  # RCCL
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    ctx = tfhe_amd.Context(args.params, local)
+    p = ctx.params
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    bk = ksk = None
+    if rank == 0:
+        sk, (bk, ksk) = ctx.keygen(42, 43, want_host_copy=want_cpu)
+    if world > 1:
+        tdist.broadcast_cloud_key(ctx, device)
+        kbuf = torch.zeros(p.n + p.N, dtype=torch.int64, device=device)
+        if rank == 0:
+            kbuf[:] = torch.from_numpy(np.concatenate([sk.key_lv0, sk.key_lv1]).astype(np.int64))
+        dist.broadcast(kbuf, 0)
+        kk = kbuf.cpu().numpy().astype(np.uint32)
+        sk = tfhe_amd.SecretKey(p, kk[:p.n], kk[p.n:])
+
+    # synthetic inputs: fresh encryptions of uniform random bits (seed 1000 + rank)
+    B = args.batch
+    g = np.random.default_rng(1000 + rank)
+    a_bits = g.integers(0, 2, B).astype(np.uint8)
+    b_bits = g.integers(0, 2, B).astype(np.uint8)
+    A = sk.encrypt_bool(a_bits, seed0=1_000_000 + rank * 10 * B)
+    Bc = sk.encrypt_bool(b_bits, seed0=5_000_000 + rank * 10 * B)
+    t_ops = torch.zeros(B, dtype=torch.uint8, device=device)  # NAND
+    t_a = torch.from_numpy(A.view(np.int32)).to(device)
+    t_b = torch.from_numpy(Bc.view(np.int32)).to(device)
+    t_o = torch.zeros_like(t_a)
+    stream = torch.cuda.current_stream(device)
+    ctx.set_stream(stream.cuda_stream)
+
+    def step():
+        ctx.gate_batch_dev(t_ops.data_ptr(), t_a.data_ptr(), t_b.data_ptr(), t_o.data_ptr(), B)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    out = t_o.cpu().numpy().view(np.uint32).copy()
+    correct = bool(np.array_equal(sk.decrypt_bool(out), ~(a_bits.astype(bool) & b_bits.astype(bool))))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    ctx.profile_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    br_ms, ks_ms, launches = ctx.profile_end()
+
+    stats = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    elapsed = float(stats[0])
+    all_correct = float(stats[1]) == 0.0
+
+    if rank == 0:
+        total = B * world * args.steps
+        value = total / elapsed
+        br_avg_s = br_ms / 1e3 / max(1, launches)
+        ks_avg_s = ks_ms / 1e3 / max(1, launches)
+        alg = algorithmic_bytes_per_gate(p) * B
+        achieved = alg / br_avg_s
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_blind_rotate_r01.json")
+        if os.path.exists(pmc_path):
+            pmc = json.load(open(pmc_path))
+            if pmc.get("batch") == B and pmc.get("params") == args.params:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "gate-bootstraps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: fresh encryptions of uniform random bits under a seeded key (sk 42, ck 43)",
+            "config": {"workload": f"{B} NAND gate bootstraps per GPU per step, SECURITY_128_BIT "
+                                   f"(n={p.n}, N={p.N}, L={p.L}, Bg=2^{p.bgbit}, t={p.iks_t})",
+                       "global_batch": B * world, "params": args.params, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK_BPS / 1e9,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_BPS, 4), "traffic": traffic,
+                         "kernel": "k_blind_rotate<3>", "kernel_avg_ms": round(br_avg_s * 1e3, 3),
+                         "algorithmic_bytes_per_launch": alg},
+            "key_switch_avg_ms": round(ks_avg_s * 1e3, 3),
+            "decrypt_check": all_correct,
+        }
+        if want_cpu:
+            line["cpu_baseline"] = cpu_baseline(p, sk, bk, ksk, A, Bc, out, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -120,6 +120,14 @@ int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *ctx, const uint8_t *ops_dev, const uin
 int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *ctx, const uint32_t *in_dev, uint32_t *out_dev,
                                  size_t B);
 
+/* ---- Device timing (HIP events on the context stream, around each kernel) */
+/* Between begin and end every bootstrap launch records events around its
+ * blind-rotation and key-switch kernels; end synchronises and returns the
+ * summed kernel milliseconds and the number of bootstrap launches. */
+int tfhe_gpu_profile_begin(tfhe_gpu_ctx *ctx);
+int tfhe_gpu_profile_end(tfhe_gpu_ctx *ctx, double *blind_rotate_ms, double *key_switch_ms,
+                         int *launches);
+
 /* ---- Stage entry points (parity tests; same kernels as the path) ------- */
 /* KlemsaProcessor.ifft1024 (fft.zig:293-366): B×N u32 -> B×N f64. */
 int tfhe_gpu_fft_forward_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, double *out, size_t B);

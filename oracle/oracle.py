@@ -25,7 +25,8 @@ class OracleParams(C.Structure):
 
 # Parameter sets, params.zig.  KSK/BSK alphas: the reference hard-wires the
 # 128-bit constants (params.zig:419-422) for every set; UINT4 keeps its own
-# (with 2e-8 BSK noise its Bg=2^22 digits would swamp the torus — DESIGN.md).
+# lv0/KSK noise and a zero BSK noise (its 2^-52 alpha is below the torus
+# resolution).
 PARAM_SETS = {
     "128": dict(n=700, N=1024, nbit=10, L=3, bgbit=6, basebit=2, iks_t=9,
                 alpha_lv0=2.0e-5, alpha_lv1=2.0e-8, alpha_ksk=2.0e-5, alpha_bsk=2.0e-8),   # :350-375
@@ -35,7 +36,7 @@ PARAM_SETS = {
                   alpha_lv0=0.00000251676160959795544987084234,
                   alpha_lv1=0.00000000000000022204460492503131,
                   alpha_ksk=0.00000251676160959795544987084234,
-                  alpha_bsk=0.00000000000000022204460492503131),                          # :210-235
+                  alpha_bsk=0.0),  # :210-235; BSK noise below torus resolution, see DESIGN.md
 }
 
 

@@ -40,6 +40,10 @@ struct tfhe_gpu_ctx {
     size_t bk_bytes = 0, ksk_bytes = 0;
     // scratch, grown on demand
     DevBuf s_a, s_b, s_out, s_lv1, s_ops, s_tv, s_tmp;
+    // device timing (tfhe_gpu_profile_begin/end): 3 events per bootstrap launch
+    bool profiling = false;
+    std::vector<hipEvent_t> events;
+    size_t ev_used = 0;
 };
 
 namespace {
@@ -118,9 +122,22 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
     int rc = ensure(c, c->s_lv1, B * 1025 * sizeof(uint32_t));
     if (rc) return rc;
     uint32_t *lv1 = key_switch ? (uint32_t *)c->s_lv1.p : out;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (c->profiling) {
+        while (c->events.size() < c->ev_used + 3) {
+            hipEvent_t e;
+            HIPCHK(c, hipEventCreate(&e));
+            c->events.push_back(e);
+        }
+        for (int i = 0; i < 3; i++) ev[i] = c->events[c->ev_used + i];
+        c->ev_used += 3;
+        HIPCHK(c, hipEventRecord(ev[0], c->stream));
+    }
     HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
                                   lv1, key_switch ? BR_OUT_LV1 : BR_OUT_TRLWE, B, c->stream));
+    if (ev[1]) HIPCHK(c, hipEventRecord(ev[1], c->stream));
     if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream));
+    if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], c->stream));
     return TFHE_OK;
 }
 
@@ -226,6 +243,7 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     for (void *p : {(void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
                     c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p})
         if (p) (void)hipFree(p);
+    for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -461,6 +479,32 @@ int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *c, const uint32_t *in_dev, uint32
     if (!c || (B && (!in_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
     HIPCHK(c, hipSetDevice(c->device));
     return run_bootstrap_dev(c, nullptr, in_dev, nullptr, nullptr, out_dev, B, true);
+}
+
+int tfhe_gpu_profile_begin(tfhe_gpu_ctx *c) {
+    if (!c) return TFHE_ERR_INVALID;
+    c->profiling = true;
+    c->ev_used = 0;
+    return TFHE_OK;
+}
+
+int tfhe_gpu_profile_end(tfhe_gpu_ctx *c, double *br_ms, double *ks_ms, int *launches) {
+    if (!c) return TFHE_ERR_INVALID;
+    c->profiling = false;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double br = 0.0, ks = 0.0;
+    for (size_t i = 0; i + 3 <= c->ev_used; i += 3) {
+        float a = 0.f, b = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&a, c->events[i], c->events[i + 1]));
+        HIPCHK(c, hipEventElapsedTime(&b, c->events[i + 1], c->events[i + 2]));
+        br += a;
+        ks += b;
+    }
+    if (br_ms) *br_ms = br;
+    if (ks_ms) *ks_ms = ks;
+    if (launches) *launches = (int)(c->ev_used / 3);
+    c->ev_used = 0;
+    return TFHE_OK;
 }
 
 int tfhe_gpu_fft_forward_batch(tfhe_gpu_ctx *c, const uint32_t *in, double *out, size_t B) {

@@ -179,12 +179,16 @@ DEV void untwist_out(C2 f, C2 w, double &tr, double &ti) {
 }
 
 // @round (half away from zero) -> i64 -> @truncate i32 -> u32 == r mod 2^32,
-// computed exactly in f64 for any finite r.
+// computed exactly in f64 for any finite r.  |r| >= 2^63 (or NaN) is
+// undefined in the reference (@intFromFloat out of range); on the x86-64
+// platform the oracle defines parity on, cvttsd2si yields
+// 0x8000000000000000, whose low word is 0 — reproduced here.  Never reached
+// by bootstrap inputs (|r| < 2^53 there).
 DEV uint32_t torus_from_f64(double v) {
     double r = round(v);
     double hi = floor(r * (1.0 / 4294967296.0));
     double lo = r - hi * 4294967296.0;
-    return (uint32_t)lo;
+    return fabs(r) < 9223372036854775808.0 ? (uint32_t)lo : 0u;
 }
 
 // decompositionIntoStorage digit (trgsw.zig:207-217); `x` already has the

@@ -49,7 +49,10 @@ SECURITY_UINT4 = dict(n=820, N=1024, nbit=10, L=1, bgbit=22, basebit=5, iks_t=3,
                       alpha_lv0=0.00000251676160959795544987084234,
                       alpha_lv1=0.00000000000000022204460492503131,
                       alpha_ksk=0.00000251676160959795544987084234,
-                      alpha_bsk=0.00000000000000022204460492503131)
+                      # 2^-52 is below the 32-bit torus resolution; the reference's
+                      # f64ToTorus would turn it into a {0,-1} bias that the
+                      # L=1/Bg=2^22 gadget amplifies 2^21x
+                      alpha_bsk=0.0)
 PARAM_SETS = {"128": SECURITY_128_BIT, "80": SECURITY_80_BIT, "uint4": SECURITY_UINT4}
 
 
@@ -79,6 +82,8 @@ _SIGS = {
     "tfhe_gpu_bootstrap_lut_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_gate_batch_dev": (C.c_int, [vp, vp, vp, vp, vp, C.c_size_t]),
     "tfhe_gpu_bootstrap_batch_dev": (C.c_int, [vp, vp, vp, C.c_size_t]),
+    "tfhe_gpu_profile_begin": (C.c_int, [vp]),
+    "tfhe_gpu_profile_end": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "tfhe_gpu_fft_forward_batch": (C.c_int, [vp, u32p, f64p, C.c_size_t]),
     "tfhe_gpu_fft_inverse_batch": (C.c_int, [vp, f64p, u32p, C.c_size_t]),
     "tfhe_gpu_poly_mul_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
@@ -211,6 +216,15 @@ class Context:
 
     def sync(self):
         self.check(self.lib.tfhe_gpu_sync(self.h), "sync")
+
+    def profile_begin(self):
+        self.check(self.lib.tfhe_gpu_profile_begin(self.h), "profile_begin")
+
+    def profile_end(self):
+        """-> (blind_rotate_ms_total, key_switch_ms_total, launches), HIP events on the ctx stream."""
+        br, ks, n = C.c_double(), C.c_double(), C.c_int()
+        self.check(self.lib.tfhe_gpu_profile_end(self.h, C.byref(br), C.byref(ks), C.byref(n)), "profile_end")
+        return br.value, ks.value, n.value
 
     # ---- batch bootstrap API
     def bootstrap_batch(self, cts):
