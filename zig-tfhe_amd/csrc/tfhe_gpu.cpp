@@ -69,7 +69,11 @@ bool params_ok(const tfhe_params *p, std::string &why) {
     if (p->n == 0 || p->n > 1024) { why = "n must be in [1, 1024]"; return false; }
     if (p->L < 1 || p->L > 3) { why = "L must be 1, 2 or 3"; return false; }
     if (p->bgbit < 1 || p->bgbit * p->L > 32) { why = "bgbit*L must be <= 32"; return false; }
-    if (p->basebit < 1 || p->basebit > 8 || p->iks_t < 1 || p->basebit * p->iks_t >= 31) {
+    // key-switch kernels are instantiated for basebit 2 with t in [7, 9]
+    // (128/80-bit) and basebit 3..8 with t in [2, 4] (Uint sets)
+    const bool ks_sel = p->basebit == 2 && p->iks_t >= 7 && p->iks_t <= 9;
+    const bool ks_gather = p->basebit >= 3 && p->basebit <= 8 && p->iks_t >= 2 && p->iks_t <= 4;
+    if (!(ks_sel || ks_gather) || p->basebit * p->iks_t >= 31) {
         why = "unsupported key-switch base/levels";
         return false;
     }
@@ -275,6 +279,7 @@ int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv
     if (rc) return rc;
     HIPCHK(c, launch_bk_permute(c->K, (const double *)c->s_tmp.p, c->d_bk, rows, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk, c->ksk_bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));  // reference leaves k=0 rows undefined
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
     return TFHE_OK;
@@ -308,6 +313,7 @@ int tfhe_gpu_import_key_device(tfhe_gpu_ctx *c, const void *bsk_dev, const void 
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->d_bk, bsk_dev, c->bk_bytes, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk_dev, c->ksk_bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
     return TFHE_OK;

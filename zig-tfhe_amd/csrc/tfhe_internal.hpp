@@ -43,6 +43,8 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
                                int out_mode, size_t B, hipStream_t s);
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
                              uint32_t *out, size_t B, hipStream_t s);
+// zero the k = 0 rows (never read by the reference; the kernels subtract them unconditionally)
+hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s);
 hipError_t launch_fft_forward(const DevTables &T, const uint32_t *in, double *out, size_t B,
                               hipStream_t s);
 hipError_t launch_fft_inverse(const DevTables &T, const double *in, uint32_t *out, size_t B,

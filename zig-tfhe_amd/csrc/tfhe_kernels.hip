@@ -121,6 +121,16 @@ DEV int swz1(int p) {
     return p ^ ((((p >> 6) & 1) * 1) ^ (((p >> 7) & 1) * 10) ^ (((p >> 8) & 1) * 4));
 }
 
+// Exchanges go through a wave-private LDS region: the LDS executes one
+// wave's DS instructions in issue order, so a wavefront-scope fence (which
+// only stops the compiler from reordering; no s_waitcnt, no s_barrier) is
+// the whole synchronisation.
+DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int NF>
 DEV void exchange1(C2 (*d)[8], C2 *xb, int t) {
     int wb = 8 * br6(t);
@@ -128,13 +138,13 @@ DEV void exchange1(C2 (*d)[8], C2 *xb, int t) {
     for (int f = 0; f < NF; f++)
 #pragma unroll
         for (int q = 0; q < 8; q++) xb[f * 512 + swz1(wb + q)] = d[f][q];
-    __syncthreads();
+    wave_sync();
     int rb = (t & 7) + 64 * (t >> 3);
 #pragma unroll
     for (int f = 0; f < NF; f++)
 #pragma unroll
         for (int q = 0; q < 8; q++) d[f][q] = xb[f * 512 + swz1(rb + 8 * q)];
-    __syncthreads();
+    wave_sync();
 }
 
 template <int NF>
@@ -144,12 +154,12 @@ DEV void exchange2(C2 (*d)[8], C2 *xb, int t) {
     for (int f = 0; f < NF; f++)
 #pragma unroll
         for (int q = 0; q < 8; q++) xb[f * 512 + wb + 8 * q] = d[f][q];
-    __syncthreads();
+    wave_sync();
 #pragma unroll
     for (int f = 0; f < NF; f++)
 #pragma unroll
         for (int q = 0; q < 8; q++) d[f][q] = xb[f * 512 + t + 64 * q];
-    __syncthreads();
+    wave_sync();
 }
 
 // 512-point radix-2 DIT (bitReverseRadix2 + radix2FFT, fft.zig:582-669) on NF
@@ -250,14 +260,17 @@ DEV void load_digits(C2 *d, const uint32_t *srcA, const uint32_t *srcB, int row,
 }
 
 // One frequency-domain multiply-accumulate row (fmaInFd1024, trgsw.zig:157-189)
-// for both output polynomials; bk = {a_re, a_im, b_re, b_im} at frequency
-// t + 64q.  `first`: the reference starts from 0.0, and 0.0 + x == x.
-DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double4 *__restrict__ bk, int t, bool first) {
+// for both output polynomials.  Device BK row layout: [q][a|b][lane] double2,
+// a = (a_re, a_im), b = (b_re, b_im) at frequency t + 64q (16-B lanes: the
+// LDS reads are conflict-free ds_read_b128).  `first`: the reference starts
+// from 0.0, and 0.0 + x == x.
+DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t, bool first) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-        double4 k = bk[q * 64 + t];
-        C2 ta = c2(d[q].x * k.x - d[q].y * k.y, d[q].x * k.y + d[q].y * k.x);
-        C2 tb = c2(d[q].x * k.z - d[q].y * k.w, d[q].x * k.w + d[q].y * k.z);
+        double2 ka = bk[(2 * q) * 64 + t];
+        double2 kb = bk[(2 * q + 1) * 64 + t];
+        C2 ta = c2(d[q].x * ka.x - d[q].y * ka.y, d[q].x * ka.y + d[q].y * ka.x);
+        C2 tb = c2(d[q].x * kb.x - d[q].y * kb.y, d[q].x * kb.y + d[q].y * kb.x);
         if (first) {
             fa[q] = ta;
             fb[q] = tb;
@@ -268,23 +281,10 @@ DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double4 *__restrict__ bk, in
     }
 }
 
-// ExternalProduct(BK row, tmp) for one TRLWE, tmp given per lane as
-// (value + offset) at coefficients t + 64m; returns the torus result added to
-// `accA/accB` (cmux: acc' = ExtProd + acc).
-template <int L>
-DEV void external_product_add(const uint32_t *tA, const uint32_t *tB, const double4 *__restrict__ bkrow,
-                              int bgbit, const LaneTw &T, const C2 *twl, C2 *xb, int t,
-                              uint32_t *accA, uint32_t *accB) {
-    C2 fa[8], fb[8];
-#pragma unroll 1
-    for (int rp = 0; rp < L; rp++) {
-        C2 d[2][8];
-        load_digits<L>(d[0], tA, tB, 2 * rp, bgbit, twl);
-        load_digits<L>(d[1], tA, tB, 2 * rp + 1, bgbit, twl);
-        fft512<2, false>(d, xb, T, t);
-        mac_row(fa, fb, d[0], bkrow + (size_t)(2 * rp) * 512, t, rp == 0);
-        mac_row(fa, fb, d[1], bkrow + (size_t)(2 * rp + 1) * 512, t, false);
-    }
+// Inverse transforms of the two accumulated spectra (fft1024 x2) and the
+// CMUX add acc' = ExtProd + acc (trgsw.zig:277-281), lane-local.
+DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const LaneTw &T, const C2 *twl, int t,
+                         uint32_t *accA, uint32_t *accB) {
     C2 e[2][8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -304,46 +304,102 @@ DEV void external_product_add(const uint32_t *tA, const uint32_t *tB, const doub
     }
 }
 
-// ---------------------------------------------------------------------------
-// Blind rotation, one wavefront per item, all n CMUX steps in one launch.
-//   acc = X^{b~} * testvec;  for i < n: acc = CMUX(BK[i], acc, X^{a~_i} acc)
-// then either sampleExtractIndex(acc, 0) (TLWELv1) or the TRLWE itself.
-// ---------------------------------------------------------------------------
+// ExternalProduct(BK row, tmp) for one TRLWE with the BK row read from global
+// memory (stage kernel); tmp per lane as (value + offset) at t + 64m.
 template <int L>
-__global__ __launch_bounds__(64, 1) void k_blind_rotate(
+DEV void external_product_add(const uint32_t *tA, const uint32_t *tB, const double2 *__restrict__ bkrow,
+                              int bgbit, const LaneTw &T, const C2 *twl, C2 *xb, int t,
+                              uint32_t *accA, uint32_t *accB) {
+    C2 fa[8], fb[8];
+#pragma unroll 1
+    for (int rp = 0; rp < L; rp++) {
+        C2 d[2][8];
+        load_digits<L>(d[0], tA, tB, 2 * rp, bgbit, twl);
+        load_digits<L>(d[1], tA, tB, 2 * rp + 1, bgbit, twl);
+        fft512<2, false>(d, xb, T, t);
+        mac_row(fa, fb, d[0], bkrow + (size_t)(2 * rp) * 1024, t, rp == 0);
+        mac_row(fa, fb, d[1], bkrow + (size_t)(2 * rp + 1) * 1024, t, false);
+    }
+    inverse_and_add(fa, fb, xb, T, twl, t, accA, accB);
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void global_void_t;
+
+// Async copy of one BK row pair (2 TRGSW rows = 32 KB, contiguous in the
+// device layout) into LDS by the whole 256-thread block: 8 x
+// global_load_lds_dwordx4 per thread, LDS destination linear.
+DEV void issue_bk_pair(const double2 *__restrict__ src, double2 *lds, int tid) {
+    const int wbase = tid & ~63;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        __builtin_amdgcn_global_load_lds((global_void_t *)(src + 256 * k + tid),
+                                         (lds_void_t *)(lds + 256 * k + wbase), 16, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// Blind rotation, one wavefront per item, 4 items per 256-thread block, all
+// n CMUX steps in one launch:
+//   acc = X^{b~} * testvec;  for i < n: acc = CMUX(BK[i], acc, X^{a~_i} acc)
+// then sampleExtractIndex(acc, 0) (TLWELv1) or the TRLWE itself.
+// The four waves consume the same BK rows, so each row pair is brought into
+// LDS once per block by LDS-DMA, issued right after the previous pair's MAC
+// and landing under the next forward FFTs.  Everything else (accumulator,
+// FFT exchanges) lives in wave-private LDS and needs no block barrier.
+// ---------------------------------------------------------------------------
+constexpr int BR_WAVES = 4;
+constexpr int BR_LDS_BK = 2048 * 16;                  // one row pair, double2
+constexpr int BR_LDS_ACC = 2048 * 4;                  // per wave
+constexpr int BR_LDS_X = 2 * 512 * 16;                // per wave, NF = 2
+constexpr int BR_LDS_AT = 1024 * 2;                   // per wave
+constexpr int BR_LDS_TOTAL = BR_LDS_BK + BR_WAVES * (BR_LDS_ACC + BR_LDS_X + BR_LDS_AT);
+
+template <int L>
+__global__ __launch_bounds__(256, 1) void k_blind_rotate(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ testvec,
-    const double4 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode) {
-    __shared__ uint32_t s_acc[2048];
-    __shared__ C2 s_x[2 * 512];
-    __shared__ uint16_t s_at[1024];
-    __shared__ int s_bt;
+    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
+    // one __shared__ array (a second one can make hipcc drain LDS-DMA early)
+    __shared__ __attribute__((aligned(16))) unsigned char smem[BR_LDS_TOTAL];
+    const int tid = threadIdx.x;
+    const int t = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    double2 *s_bk = reinterpret_cast<double2 *>(smem);
+    uint32_t *s_acc = reinterpret_cast<uint32_t *>(smem + BR_LDS_BK + w * BR_LDS_ACC);
+    C2 *s_x = reinterpret_cast<C2 *>(smem + BR_LDS_BK + BR_WAVES * BR_LDS_ACC + w * BR_LDS_X);
+    uint16_t *s_at = reinterpret_cast<uint16_t *>(smem + BR_LDS_BK + BR_WAVES * (BR_LDS_ACC + BR_LDS_X) +
+                                                  w * BR_LDS_AT);
 
-    const int t = threadIdx.x;
-    const size_t g = blockIdx.x;
     const int n = P.n;
+    const size_t g_raw = (size_t)blockIdx.x * BR_WAVES + w;
+    const bool valid = g_raw < B;
+    const size_t g = valid ? g_raw : B - 1;  // ragged tail: compute a copy, store nothing
     const uint32_t *A = in_a + g * (size_t)(n + 1);
     const uint32_t *Bv = in_b ? in_b + g * (size_t)(n + 1) : A;
     const int op = ops ? (int)ops[g] : 255;
+    const size_t row_pair = 2048;                     // double2 per BK row pair
+    const size_t step_stride = (size_t)L * row_pair;  // double2 per TRGSW (BK[i])
+
+    issue_bk_pair(bkd, s_bk, tid);  // pair (0, 0), lands under the prologue
 
     // a~_i = (a_i + 2^20) >> 21 and b~ = 2N - ((b + 2^20) >> 21), 64-bit adds
     // (trgsw.zig:297, :312).
+    int bt = 0;
     for (int i = t; i <= n; i += 64) {
         uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
         uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
         if (i < n) s_at[i] = (uint16_t)tl;
-        else s_bt = 2048 - (int)tl;
+        else bt = 2048 - (int)tl;
     }
+    bt = __builtin_amdgcn_readlane(bt, n & 63);
     LaneTw T;
     load_lane_tw(T, TT.tw, t);
     C2 twl[8];
 #pragma unroll
     for (int m = 0; m < 8; m++) twl[m] = TT.twist[t + 64 * m];
-    __syncthreads();
 
     // acc = X^{b~} * testvec (trgsw.zig:300-306), lane owns k = t + 64m.
     uint32_t accA[16], accB[16];
-    const int bt = s_bt;
 #pragma unroll
     for (int m = 0; m < 16; m++) {
         accA[m] = rot_read(testvec, t + 64 * m, bt);
@@ -351,31 +407,42 @@ __global__ __launch_bounds__(64, 1) void k_blind_rotate(
         s_acc[t + 64 * m] = accA[m];
         s_acc[1024 + t + 64 * m] = accB[m];
     }
-    __syncthreads();
+    wave_sync();
 
-    const size_t row_stride = (size_t)2 * L * 512;  // double4 per BK row (TRGSW)
     for (int i = 0; i < n; i++) {
-        const int at = s_at[i];
-        // a~ in {0, 2N}: rot == acc, tmp == 0, every digit is 0 and the
-        // external product is exactly 0 -> the step is an exact no-op.
-        if (at == 0 || at == 2048) continue;
+        // a~ in {0, 2N} gives tmp = 0 and an exactly-zero external product;
+        // it is computed anyway so the four waves keep one barrier schedule.
+        const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
         uint32_t tA[16], tB[16];
 #pragma unroll
         for (int m = 0; m < 16; m++) {
             tA[m] = rot_read(s_acc, t + 64 * m, at) - accA[m] + P.offset;
             tB[m] = rot_read(s_acc + 1024, t + 64 * m, at) - accB[m] + P.offset;
         }
-        external_product_add<L>(tA, tB, bkd + (size_t)i * row_stride, P.bgbit, T, twl, s_x, t, accA,
-                                accB);
-        __syncthreads();  // all lanes done reading the old accumulator
+        C2 fa[8], fb[8];
+#pragma unroll 1
+        for (int rp = 0; rp < L; rp++) {
+            C2 d[2][8];
+            load_digits<L>(d[0], tA, tB, 2 * rp, P.bgbit, twl);
+            load_digits<L>(d[1], tA, tB, 2 * rp + 1, P.bgbit, twl);
+            fft512<2, false>(d, s_x, T, t);
+            __syncthreads();  // BK pair (i, rp) has landed (s_waitcnt vmcnt(0) + s_barrier)
+            mac_row(fa, fb, d[0], s_bk, t, rp == 0);
+            mac_row(fa, fb, d[1], s_bk + 1024, t, false);
+            __syncthreads();  // every wave is done reading the pair
+            const size_t nxt = (size_t)i * step_stride + (size_t)(rp + 1) * row_pair;
+            if (rp + 1 < L || i + 1 < n) issue_bk_pair(bkd + nxt, s_bk, tid);
+        }
+        inverse_and_add(fa, fb, s_x, T, twl, t, accA, accB);
 #pragma unroll
         for (int m = 0; m < 16; m++) {
             s_acc[t + 64 * m] = accA[m];
             s_acc[1024 + t + 64 * m] = accB[m];
         }
-        __syncthreads();
+        wave_sync();
     }
 
+    if (!valid) return;
     if (out_mode == BR_OUT_LV1) {
         // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
         uint32_t *o = out + g * (size_t)1025;
@@ -393,45 +460,127 @@ __global__ __launch_bounds__(64, 1) void k_blind_rotate(
 }
 
 // ---------------------------------------------------------------------------
-// Identity key switching (trgsw.zig:471-502).  Block = 256 output words x G
-// items; per (i, j) every item picks row k of the 2^basebit candidates; the
-// candidates are shared by the G items through L1.
+// Identity key switching (trgsw.zig:471-502):
+//   res = (0,...,0, b) - sum_{i<N, j<t} KSK[i][j][digit_j(a_i + 2^(32-(1+basebit*t)))]
+// Integer gather-subtract; the k = 0 rows of the device KSK are zero (the
+// reference skips them, trgsw.zig:490), so every (i, j) subtracts
+// unconditionally.  Lane = output word (n+1 words per item), G items per
+// block.  All t digits of a_i are the top basebit*t bits of a_i + prec, so
+// one shift gives them packed.
 // ---------------------------------------------------------------------------
-template <int G>
-__global__ __launch_bounds__(256) void k_key_switch(KParams P, const uint32_t *__restrict__ lv1,
-                                                    const uint32_t *__restrict__ ksk,
-                                                    uint32_t *__restrict__ out, size_t B) {
-    __shared__ uint32_t s_in[G][1025];
+// Select form (2^basebit <= 4): per (i, j) a lane loads the 3 non-zero
+// candidate words once; each of the G items then picks its word by its
+// wave-uniform digit (readlane -> SGPR), so KSK traffic is per block, not per
+// item.
+template <int T, int G>
+__global__ __launch_bounds__(256) void k_key_switch_sel(KParams P, const uint32_t *__restrict__ lv1,
+                                                        const uint32_t *__restrict__ ksk,
+                                                        uint32_t *__restrict__ out, size_t B) {
     const size_t g0 = (size_t)blockIdx.y * G;
     const int w = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int n1 = P.n + 1;
-    for (int x = threadIdx.x; x < G * 1025; x += 256) {
-        int gi = x / 1025, e = x % 1025;
-        s_in[gi][e] = (g0 + gi < B) ? lv1[(g0 + gi) * 1025 + e] : 0u;
-    }
-    __syncthreads();
+    const bool active = w < n1;
+    const int wc = active ? w : 0;
     uint32_t res[G];
 #pragma unroll
-    for (int gi = 0; gi < G; gi++) res[gi] = (w == P.n) ? s_in[gi][1024] : 0u;
-    const int basebit = P.basebit, T = P.iks_t, base = 1 << basebit;
-    const uint32_t prec = 1u << (32 - (1 + basebit * T));
-    const bool active = w < n1;
-    for (int i = 0; i < 1024; i++) {
-        const uint32_t *rows_i = ksk + (size_t)base * T * i * n1;
-        for (int j = 0; j < T; j++) {
-            const int sh = 32 - (j + 1) * basebit;
+    for (int g = 0; g < G; g++) res[g] = (w == P.n && g0 + g < B) ? lv1[(g0 + g) * 1025 + 1024] : 0u;
+    const uint32_t prec = 1u << (32 - (1 + 2 * T));
+    const size_t stride_i = (size_t)T * 4 * n1;
+    const uint32_t *rows0 = ksk + wc;
+    for (int i0 = 0; i0 < 1024; i0 += 64) {
+        // packed digits of a_{i0+lane} for every item: pkv[g] in lane l is item g's i0+l
+        uint32_t pkv[G];
 #pragma unroll
-            for (int gi = 0; gi < G; gi++) {
-                uint32_t k = ((s_in[gi][i] + prec) >> sh) & (uint32_t)(base - 1);
-                if (k != 0 && active) res[gi] -= rows_i[((size_t)base * j + k) * n1 + w];
+        for (int g = 0; g < G; g++) {
+            const uint32_t a = (g0 + g < B) ? lv1[(g0 + g) * 1025 + i0 + lane] : 0u;
+            pkv[g] = (a + prec) >> (32 - 2 * T);  // digit j at bits 2(T-1-j)
+        }
+        for (int ii = 0; ii < 64; ii++) {
+            const uint32_t *rows = rows0 + (size_t)(i0 + ii) * stride_i;
+            uint32_t r[T][3];
+#pragma unroll
+            for (int j = 0; j < T; j++)
+#pragma unroll
+                for (int k = 0; k < 3; k++) r[j][k] = rows[(size_t)(4 * j + k + 1) * n1];
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const uint32_t pk = __builtin_amdgcn_readlane(pkv[g], ii);
+#pragma unroll
+                for (int j = 0; j < T; j++) {
+                    const uint32_t k = (pk >> (2 * (T - 1 - j))) & 3u;
+                    const uint32_t v = (k & 2u) ? ((k & 1u) ? r[j][2] : r[j][1]) : ((k & 1u) ? r[j][0] : 0u);
+                    res[g] -= v;
+                }
             }
         }
     }
     if (active) {
 #pragma unroll
-        for (int gi = 0; gi < G; gi++)
-            if (g0 + gi < B) out[(g0 + gi) * n1 + w] = res[gi];
+        for (int g = 0; g < G; g++)
+            if (g0 + g < B) out[(g0 + g) * n1 + w] = res[g];
     }
+}
+
+// Gather form (any base): per (i, j) each item loads its selected row word;
+// the G*t loads of one i are independent and issued together (no branches),
+// candidates are shared across the block's items through L1/L2.
+template <int T, int G>
+__global__ __launch_bounds__(256) void k_key_switch_gather(KParams P, const uint32_t *__restrict__ lv1,
+                                                           const uint32_t *__restrict__ ksk,
+                                                           uint32_t *__restrict__ out, size_t B) {
+    const size_t g0 = (size_t)blockIdx.y * G;
+    const int w = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int n1 = P.n + 1;
+    const bool active = w < n1;
+    const int wc = active ? w : 0;
+    const int basebit = P.basebit, base = 1 << basebit;
+    uint32_t res[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) res[g] = (w == P.n && g0 + g < B) ? lv1[(g0 + g) * 1025 + 1024] : 0u;
+    const uint32_t prec = 1u << (32 - (1 + basebit * T));
+    const size_t stride_i = (size_t)T * base * n1;
+    const uint32_t *rows0 = ksk + wc;
+    for (int i0 = 0; i0 < 1024; i0 += 64) {
+        uint32_t pkv[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const uint32_t a = (g0 + g < B) ? lv1[(g0 + g) * 1025 + i0 + lane] : 0u;
+            pkv[g] = (a + prec) >> (32 - basebit * T);
+        }
+#pragma unroll 2
+        for (int ii = 0; ii < 64; ii++) {
+            const uint32_t *rows = rows0 + (size_t)(i0 + ii) * stride_i;
+            uint32_t v[G][T];
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const uint32_t pk = __builtin_amdgcn_readlane(pkv[g], ii);
+#pragma unroll
+                for (int j = 0; j < T; j++) {
+                    const uint32_t k = (pk >> (basebit * (T - 1 - j))) & (uint32_t)(base - 1);
+                    v[g][j] = rows[(size_t)(base * j + k) * n1];
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; g++)
+#pragma unroll
+                for (int j = 0; j < T; j++) res[g] -= v[g][j];
+        }
+    }
+    if (active) {
+#pragma unroll
+        for (int g = 0; g < G; g++)
+            if (g0 + g < B) out[(g0 + g) * n1 + w] = res[g];
+    }
+}
+
+// Zero the k = 0 rows of a KSK (left undefined by the reference, key.zig:156).
+__global__ void k_ksk_zero_k0(uint32_t *__restrict__ ksk, int n1, int base, size_t groups) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= groups * n1) return;
+    size_t grp = idx / n1, x = idx % n1;
+    ksk[grp * base * n1 + x] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -535,7 +684,7 @@ __global__ __launch_bounds__(64) void k_poly_mul(DevTables TT, const uint32_t *_
 // device-layout TRGSW row.
 template <int L>
 __global__ __launch_bounds__(64) void k_external_product(KParams P, DevTables TT,
-                                                         const double4 *__restrict__ bkrow,
+                                                         const double2 *__restrict__ bkrow,
                                                          const uint32_t *__restrict__ in,
                                                          uint32_t *__restrict__ out) {
     __shared__ C2 s_x[2 * 512];
@@ -563,9 +712,9 @@ __global__ __launch_bounds__(64) void k_external_product(KParams P, DevTables TT
     }
 }
 
-// BK layout permutation: ref [rows][2][1024] (a|b, each re[512] ++ im[512])
-// <-> device [rows][8][64] double4 {a_re, a_im, b_re, b_im} at freq t + 64q.
-__global__ void k_bk_permute(const double *__restrict__ ref, double4 *__restrict__ dev, size_t rows,
+// BK layout permutation: reference [rows][a|b][1024] (each re[512] ++ im[512])
+// <-> device [rows][q][a|b][64] double2 (re, im) at frequency t + 64q.
+__global__ void k_bk_permute(const double *__restrict__ ref, double2 *__restrict__ dev, size_t rows,
                              int dir) {
     size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= rows * 512) return;
@@ -573,21 +722,18 @@ __global__ void k_bk_permute(const double *__restrict__ ref, double4 *__restrict
     int pos = (int)(idx % 512);
     int q = pos >> 6, t = pos & 63;  // pos = t + 64q
     const size_t rb = row * 2048;
-    double4 *dp = dev + row * 512 + (size_t)q * 64 + t;
+    double2 *da = dev + row * 1024 + (size_t)(2 * q) * 64 + t;
+    double2 *db = da + 64;
     if (dir == 0) {
-        double4 v;
-        v.x = ref[rb + pos];
-        v.y = ref[rb + 512 + pos];
-        v.z = ref[rb + 1024 + pos];
-        v.w = ref[rb + 1536 + pos];
-        *dp = v;
+        *da = make_double2(ref[rb + pos], ref[rb + 512 + pos]);
+        *db = make_double2(ref[rb + 1024 + pos], ref[rb + 1536 + pos]);
     } else {
-        double4 v = *dp;
         double *r = const_cast<double *>(ref);
-        r[rb + pos] = v.x;
-        r[rb + 512 + pos] = v.y;
-        r[rb + 1024 + pos] = v.z;
-        r[rb + 1536 + pos] = v.w;
+        double2 a = *da, b = *db;
+        r[rb + pos] = a.x;
+        r[rb + 512 + pos] = a.y;
+        r[rb + 1024 + pos] = b.x;
+        r[rb + 1536 + pos] = b.y;
     }
 }
 
@@ -599,20 +745,20 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
                                const double *bkd, uint32_t *out, int out_mode, size_t B,
                                hipStream_t s) {
     if (B == 0) return hipSuccess;
-    dim3 grid((unsigned)B), block(64);
-    const double4 *bk4 = reinterpret_cast<const double4 *>(bkd);
+    dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(64 * BR_WAVES);
+    const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
     switch (P.L) {
     case 1:
-        hipLaunchKernelGGL(k_blind_rotate<1>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk4, out,
-                           out_mode);
+        hipLaunchKernelGGL(k_blind_rotate<1>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out,
+                           out_mode, B);
         break;
     case 2:
-        hipLaunchKernelGGL(k_blind_rotate<2>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk4, out,
-                           out_mode);
+        hipLaunchKernelGGL(k_blind_rotate<2>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out,
+                           out_mode, B);
         break;
     case 3:
-        hipLaunchKernelGGL(k_blind_rotate<3>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk4, out,
-                           out_mode);
+        hipLaunchKernelGGL(k_blind_rotate<3>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out,
+                           out_mode, B);
         break;
     default:
         return hipErrorInvalidValue;
@@ -623,9 +769,48 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk, uint32_t *out,
                              size_t B, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    constexpr int G = 8;
+    // items per block: development knob TFHE_KS_G in {8, 16, 32} (default 8)
+    static const int G = [] {
+        const char *e = getenv("TFHE_KS_G");
+        int v = e ? atoi(e) : 8;
+        return (v == 16 || v == 32) ? v : 8;
+    }();
     dim3 grid((unsigned)((P.n + 1 + 255) / 256), (unsigned)((B + G - 1) / G)), block(256);
-    hipLaunchKernelGGL(k_key_switch<G>, grid, block, 0, s, P, lv1, ksk, out, B);
+#define KS_SEL(T_, G_) hipLaunchKernelGGL((k_key_switch_sel<T_, G_>), grid, block, 0, s, P, lv1, ksk, out, B)
+#define KS_GATHER(T_, G_) hipLaunchKernelGGL((k_key_switch_gather<T_, G_>), grid, block, 0, s, P, lv1, ksk, out, B)
+#define KS_G(KIND, T_)                  \
+    do {                                \
+        if (G == 16) KIND(T_, 16);      \
+        else if (G == 32) KIND(T_, 32); \
+        else KIND(T_, 8);               \
+    } while (0)
+    if (P.basebit == 2) {
+        switch (P.iks_t) {
+        case 7: KS_G(KS_SEL, 7); break;
+        case 8: KS_G(KS_SEL, 8); break;
+        case 9: KS_G(KS_SEL, 9); break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (P.iks_t) {
+        case 2: KS_G(KS_GATHER, 2); break;
+        case 3: KS_G(KS_GATHER, 3); break;
+        case 4: KS_G(KS_GATHER, 4); break;
+        default: return hipErrorInvalidValue;
+        }
+    }
+#undef KS_SEL
+#undef KS_GATHER
+#undef KS_G
+    return hipGetLastError();
+}
+
+hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s) {
+    const int n1 = P.n + 1, base = 1 << P.basebit;
+    const size_t groups = (size_t)1024 * P.iks_t;
+    const size_t total = groups * n1;
+    hipLaunchKernelGGL(k_ksk_zero_k0, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ksk, n1, base,
+                       groups);
     return hipGetLastError();
 }
 
@@ -651,11 +836,11 @@ hipError_t launch_poly_mul(const DevTables &T, const uint32_t *a, const uint32_t
 hipError_t launch_external_product(const KParams &P, const DevTables &T, const double *bkd_row,
                                    const uint32_t *in, uint32_t *out, size_t B, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    const double4 *bk4 = reinterpret_cast<const double4 *>(bkd_row);
+    const double2 *bk2 = reinterpret_cast<const double2 *>(bkd_row);
     switch (P.L) {
-    case 1: hipLaunchKernelGGL(k_external_product<1>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk4, in, out); break;
-    case 2: hipLaunchKernelGGL(k_external_product<2>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk4, in, out); break;
-    case 3: hipLaunchKernelGGL(k_external_product<3>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk4, in, out); break;
+    case 1: hipLaunchKernelGGL(k_external_product<1>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk2, in, out); break;
+    case 2: hipLaunchKernelGGL(k_external_product<2>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk2, in, out); break;
+    case 3: hipLaunchKernelGGL(k_external_product<3>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk2, in, out); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -665,7 +850,7 @@ hipError_t launch_bk_permute(const KParams &, const double *bk_ref, double *bkd,
     size_t total = rows * 512;
     if (!total) return hipSuccess;
     hipLaunchKernelGGL(k_bk_permute, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, bk_ref,
-                       reinterpret_cast<double4 *>(bkd), rows, 0);
+                       reinterpret_cast<double2 *>(bkd), rows, 0);
     return hipGetLastError();
 }
 
@@ -673,7 +858,7 @@ hipError_t launch_bk_unpermute(const KParams &, const double *bkd, double *bk_re
     size_t total = rows * 512;
     if (!total) return hipSuccess;
     hipLaunchKernelGGL(k_bk_permute, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, bk_ref,
-                       reinterpret_cast<double4 *>(const_cast<double *>(bkd)), rows, 1);
+                       reinterpret_cast<double2 *>(const_cast<double *>(bkd)), rows, 1);
     return hipGetLastError();
 }
 
