@@ -66,52 +66,79 @@ DEV void bf1(C2 &u, C2 &x) {
 DEV int br3(int q) { return ((q & 1) << 2) | (q & 2) | ((q >> 2) & 1); }
 DEV int br6(int t) { return (int)(__builtin_bitreverse32((uint32_t)t) >> 26); }
 
-// Per-lane twiddles.  Table index of stage len, j: len/2 - 1 + j.
-struct LaneTw {
-    C2 w4, w8_1, w8_2, w8_3;       // pass A (lane-uniform)
-    C2 w16, w32[2], w64[4];        // pass B, j = (t&7) + 8*...
-    C2 w128, w256[2], w512[4];     // pass C, j = t + 64*...
+// Stage twiddles.  Table index of stage len, j: len/2 - 1 + j.
+//   pass A (len 4, 8):     W4[1], W8[1..3]                   lane-uniform
+//   pass B (len 16..64):   W16[r], W32[r + 8k], W64[r + 8k]  r = t & 7
+//   pass C (len 128..512): W128[t], W256[t+64k], W512[t+64k]
+// Two providers: RegTw keeps all of them in registers (single-wave stage
+// kernels), LdsTw reads passes B/C from a block-shared LDS copy of the table
+// when a pass starts (blind rotation: frees ~60 VGPRs per lane).
+DEV void tw_pass_b(C2 *w, const C2 *tw, int t) {
+    const int r = t & 7;
+    w[0] = tw[7 + r];
+    w[1] = tw[15 + r];
+    w[2] = tw[15 + r + 8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[3 + k] = tw[31 + r + 8 * k];
+}
+DEV void tw_pass_c(C2 *w, const C2 *tw, int t) {
+    w[0] = tw[63 + t];
+    w[1] = tw[127 + t];
+    w[2] = tw[127 + t + 64];
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[3 + k] = tw[255 + t + 64 * k];
+}
+
+struct RegTw {
+    C2 a[4], b[7], c[7];
+    DEV void init(const C2 *__restrict__ tw, int t) {
+        a[0] = tw[2];
+        a[1] = tw[4];
+        a[2] = tw[5];
+        a[3] = tw[6];
+        tw_pass_b(b, tw, t);
+        tw_pass_c(c, tw, t);
+    }
+    DEV void pass_b(C2 *w, int) const {
+#pragma unroll
+        for (int k = 0; k < 7; k++) w[k] = b[k];
+    }
+    DEV void pass_c(C2 *w, int) const {
+#pragma unroll
+        for (int k = 0; k < 7; k++) w[k] = c[k];
+    }
 };
 
-DEV void load_lane_tw(LaneTw &T, const C2 *__restrict__ tw, int t) {
-    T.w4 = tw[2];
-    T.w8_1 = tw[4];
-    T.w8_2 = tw[5];
-    T.w8_3 = tw[6];
-    int r = t & 7;
-    T.w16 = tw[7 + r];
-    T.w32[0] = tw[15 + r];
-    T.w32[1] = tw[15 + r + 8];
-#pragma unroll
-    for (int q = 0; q < 4; q++) T.w64[q] = tw[31 + r + 8 * q];
-    T.w128 = tw[63 + t];
-    T.w256[0] = tw[127 + t];
-    T.w256[1] = tw[127 + t + 64];
-#pragma unroll
-    for (int q = 0; q < 4; q++) T.w512[q] = tw[255 + t + 64 * q];
-}
+struct LdsTw {
+    C2 a[4];
+    const C2 *tw;  // LDS copy of the stage table
+    DEV void init(const C2 *lds_tw) {
+        tw = lds_tw;
+        a[0] = tw[2];
+        a[1] = tw[4];
+        a[2] = tw[5];
+        a[3] = tw[6];
+    }
+    DEV void pass_b(C2 *w, int t) const { tw_pass_b(w, tw, t); }
+    DEV void pass_c(C2 *w, int t) const { tw_pass_c(w, tw, t); }
+};
 
 // Pass A: stages len = 2, 4, 8 (bits 0-2 of the bit-reversed position are the
 // register index q).
 template <bool INV>
-DEV void passA(C2 *d, const LaneTw &T) {
+DEV void passA(C2 *d, const C2 *a) {
     bf1(d[0], d[1]); bf1(d[2], d[3]); bf1(d[4], d[5]); bf1(d[6], d[7]);
-    bf1(d[0], d[2]); bf<INV>(d[1], d[3], T.w4); bf1(d[4], d[6]); bf<INV>(d[5], d[7], T.w4);
-    bf1(d[0], d[4]); bf<INV>(d[1], d[5], T.w8_1); bf<INV>(d[2], d[6], T.w8_2); bf<INV>(d[3], d[7], T.w8_3);
+    bf1(d[0], d[2]); bf<INV>(d[1], d[3], a[0]); bf1(d[4], d[6]); bf<INV>(d[5], d[7], a[0]);
+    bf1(d[0], d[4]); bf<INV>(d[1], d[5], a[1]); bf<INV>(d[2], d[6], a[2]); bf<INV>(d[3], d[7], a[3]);
 }
 // Pass B: stages 16, 32, 64 (position bits 3-5 in q; j = (t&7) + 8*(...)).
-template <bool INV>
-DEV void passB(C2 *d, const LaneTw &T) {
-    bf<INV>(d[0], d[1], T.w16); bf<INV>(d[2], d[3], T.w16); bf<INV>(d[4], d[5], T.w16); bf<INV>(d[6], d[7], T.w16);
-    bf<INV>(d[0], d[2], T.w32[0]); bf<INV>(d[1], d[3], T.w32[1]); bf<INV>(d[4], d[6], T.w32[0]); bf<INV>(d[5], d[7], T.w32[1]);
-    bf<INV>(d[0], d[4], T.w64[0]); bf<INV>(d[1], d[5], T.w64[1]); bf<INV>(d[2], d[6], T.w64[2]); bf<INV>(d[3], d[7], T.w64[3]);
-}
 // Pass C: stages 128, 256, 512 (position bits 6-8 in q; j = t + 64*(...)).
+// w = {W_s1, W_s2[0..1], W_s3[0..3]} of the pass's three stages.
 template <bool INV>
-DEV void passC(C2 *d, const LaneTw &T) {
-    bf<INV>(d[0], d[1], T.w128); bf<INV>(d[2], d[3], T.w128); bf<INV>(d[4], d[5], T.w128); bf<INV>(d[6], d[7], T.w128);
-    bf<INV>(d[0], d[2], T.w256[0]); bf<INV>(d[1], d[3], T.w256[1]); bf<INV>(d[4], d[6], T.w256[0]); bf<INV>(d[5], d[7], T.w256[1]);
-    bf<INV>(d[0], d[4], T.w512[0]); bf<INV>(d[1], d[5], T.w512[1]); bf<INV>(d[2], d[6], T.w512[2]); bf<INV>(d[3], d[7], T.w512[3]);
+DEV void passBC(C2 *d, const C2 *w) {
+    bf<INV>(d[0], d[1], w[0]); bf<INV>(d[2], d[3], w[0]); bf<INV>(d[4], d[5], w[0]); bf<INV>(d[6], d[7], w[0]);
+    bf<INV>(d[0], d[2], w[1]); bf<INV>(d[1], d[3], w[2]); bf<INV>(d[4], d[6], w[1]); bf<INV>(d[5], d[7], w[2]);
+    bf<INV>(d[0], d[4], w[3]); bf<INV>(d[1], d[5], w[4]); bf<INV>(d[2], d[6], w[5]); bf<INV>(d[3], d[7], w[6]);
 }
 
 // Exchange 1 (after pass A): lane t wrote positions 8*br6(t)+q, reads
@@ -165,16 +192,77 @@ DEV void exchange2(C2 (*d)[8], C2 *xb, int t) {
 // 512-point radix-2 DIT (bitReverseRadix2 + radix2FFT, fft.zig:582-669) on NF
 // transforms at once.  In: d[f][q] = z[t + 64*br3(q)] (the bit reversal is
 // absorbed into the load order).  Out: d[f][q] = Z[t + 64q].
-template <int NF, bool INV>
-DEV void fft512(C2 (*d)[8], C2 *xb, const LaneTw &T, int t) {
+// Exchange halves for one transform: write its registers to its region
+// (xb already offset to it), or read the next layout back.
+DEV void ex1_write(const C2 *d, C2 *xb, int t) {
+    const int wb = 8 * br6(t);
 #pragma unroll
-    for (int f = 0; f < NF; f++) passA<INV>(d[f], T);
+    for (int q = 0; q < 8; q++) xb[swz1(wb + q)] = d[q];
+}
+DEV void ex1_read(C2 *d, const C2 *xb, int t) {
+    const int rb = (t & 7) + 64 * (t >> 3);
+#pragma unroll
+    for (int q = 0; q < 8; q++) d[q] = xb[swz1(rb + 8 * q)];
+}
+DEV void ex2_write(const C2 *d, C2 *xb, int t) {
+    const int wb = (t & 7) + 64 * (t >> 3);
+#pragma unroll
+    for (int q = 0; q < 8; q++) xb[wb + 8 * q] = d[q];
+}
+DEV void ex2_read(C2 *d, const C2 *xb, int t) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) d[q] = xb[t + 64 * q];
+}
+
+// Two independent transforms, software-pipelined so that each transform's
+// LDS exchange (write burst, in-order read-back) overlaps the other one's
+// butterfly pass: the wave always has VALU work while its DS queue drains.
+// Same arithmetic as fft512<2, INV>.
+template <bool INV, class TW>
+DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
+    C2 *x0 = xb, *x1 = xb + 512;
+    C2 wb_[7], wc_[7];
+    passA<INV>(d[0], T.a);
+    ex1_write(d[0], x0, t);
+    wave_sync();
+    passA<INV>(d[1], T.a);
+    ex1_read(d[0], x0, t);
+    ex1_write(d[1], x1, t);
+    wave_sync();
+    T.pass_b(wb_, t);
+    passBC<INV>(d[0], wb_);
+    ex1_read(d[1], x1, t);
+    ex2_write(d[0], x0, t);
+    wave_sync();
+    passBC<INV>(d[1], wb_);
+    T.pass_c(wc_, t);
+    ex2_read(d[0], x0, t);
+    ex2_write(d[1], x1, t);
+    wave_sync();
+    passBC<INV>(d[0], wc_);
+    ex2_read(d[1], x1, t);
+    wave_sync();
+    passBC<INV>(d[1], wc_);
+}
+
+template <int NF, bool INV, class TW>
+DEV void fft512(C2 (*d)[8], C2 *xb, const TW &T, int t) {
+#pragma unroll
+    for (int f = 0; f < NF; f++) passA<INV>(d[f], T.a);
     exchange1<NF>(d, xb, t);
+    {
+        C2 w[7];
+        T.pass_b(w, t);
 #pragma unroll
-    for (int f = 0; f < NF; f++) passB<INV>(d[f], T);
+        for (int f = 0; f < NF; f++) passBC<INV>(d[f], w);
+    }
     exchange2<NF>(d, xb, t);
+    {
+        C2 w[7];
+        T.pass_c(w, t);
 #pragma unroll
-    for (int f = 0; f < NF; f++) passC<INV>(d[f], T);
+        for (int f = 0; f < NF; f++) passBC<INV>(d[f], w);
+    }
 }
 
 // Fold + twist of ifft1024 (fft.zig:301-323): z = (x_re, x_im) * twist.
@@ -199,6 +287,23 @@ DEV uint32_t torus_from_f64(double v) {
     double hi = floor(r * (1.0 / 4294967296.0));
     double lo = r - hi * 4294967296.0;
     return fabs(r) < 9223372036854775808.0 ? (uint32_t)lo : 0u;
+}
+
+// Same result in 8 VALU ops when |v| < 2^51 is guaranteed by the parameter
+// set (|ExtProd| <= 2L * N * Bg/2 * 2^31; 2^47.6 at L=3, Bg=2^6): trunc,
+// then t + 1.5*2^52 is exact and its low mantissa word is t mod 2^32.
+DEV uint32_t torus_from_f64_small(double v) {
+    const double t = trunc(v);
+    const double frac = v - t;  // exact
+    const double s = t + 6755399441055744.0;
+    const uint32_t lo = (uint32_t)__double_as_longlong(s);
+    const uint32_t adj = fabs(frac) >= 0.5 ? (v < 0.0 ? 0xFFFFFFFFu : 1u) : 0u;
+    return lo + adj;
+}
+
+template <bool SMALL>
+DEV uint32_t to_torus(double v) {
+    return SMALL ? torus_from_f64_small(v) : torus_from_f64(v);
 }
 
 // decompositionIntoStorage digit (trgsw.zig:207-217); `x` already has the
@@ -241,37 +346,34 @@ DEV uint32_t gate_combine(int op, uint32_t x, uint32_t y, bool is_b) {
     return r;
 }
 
-// Load an fft512 input pair from the decomposed accumulator difference.
-// src[m] holds (rot - acc + offset) at coefficient t + 64m, m < 16.
-// `row` may be a runtime value: the a/b source is chosen per element by a
-// select, never by indexing a register array dynamically (no scratch).
-template <int L>
-DEV void load_digits(C2 *d, const uint32_t *srcA, const uint32_t *srcB, int row, int bgbit,
-                     const C2 *twl) {
-    const bool from_a = row < L;
-    const int level = from_a ? row : row - L;
+// Load an fft512 input (one decomposition row, compile-time) from the
+// accumulator difference: src[m] = (rot - acc + offset) at coefficient
+// t + 64m, m < 16.  Twist factor of coefficient t + 64m at tws[m * TS].
+template <int L, int ROW, int TS>
+DEV void load_digits(C2 *d, const uint32_t *srcA, const uint32_t *srcB, int bgbit, const C2 *tws) {
+    const uint32_t *src = ROW < L ? srcA : srcB;
+    constexpr int level = ROW < L ? ROW : ROW - L;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-        int m = br3(q);
-        uint32_t re = from_a ? srcA[m] : srcB[m];
-        uint32_t im = from_a ? srcA[m + 8] : srcB[m + 8];
-        d[q] = twist_in(digit_f64(re, level, bgbit), digit_f64(im, level, bgbit), twl[m]);
+        const int m = br3(q);
+        d[q] = twist_in(digit_f64(src[m], level, bgbit), digit_f64(src[m + 8], level, bgbit), tws[m * TS]);
     }
 }
 
 // One frequency-domain multiply-accumulate row (fmaInFd1024, trgsw.zig:157-189)
 // for both output polynomials.  Device BK row layout: [q][a|b][lane] double2,
 // a = (a_re, a_im), b = (b_re, b_im) at frequency t + 64q (16-B lanes: the
-// LDS reads are conflict-free ds_read_b128).  `first`: the reference starts
+// LDS reads are conflict-free ds_read_b128).  FIRST: the reference starts
 // from 0.0, and 0.0 + x == x.
-DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t, bool first) {
+template <bool FIRST>
+DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-        double2 ka = bk[(2 * q) * 64 + t];
-        double2 kb = bk[(2 * q + 1) * 64 + t];
-        C2 ta = c2(d[q].x * ka.x - d[q].y * ka.y, d[q].x * ka.y + d[q].y * ka.x);
-        C2 tb = c2(d[q].x * kb.x - d[q].y * kb.y, d[q].x * kb.y + d[q].y * kb.x);
-        if (first) {
+        const double2 ka = bk[(2 * q) * 64 + t];
+        const double2 kb = bk[(2 * q + 1) * 64 + t];
+        const C2 ta = c2(d[q].x * ka.x - d[q].y * ka.y, d[q].x * ka.y + d[q].y * ka.x);
+        const C2 tb = c2(d[q].x * kb.x - d[q].y * kb.y, d[q].x * kb.y + d[q].y * kb.x);
+        if (FIRST) {
             fa[q] = ta;
             fb[q] = tb;
         } else {
@@ -283,7 +385,8 @@ DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t, bool fir
 
 // Inverse transforms of the two accumulated spectra (fft1024 x2) and the
 // CMUX add acc' = ExtProd + acc (trgsw.zig:277-281), lane-local.
-DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const LaneTw &T, const C2 *twl, int t,
+template <bool SMALL, int TS, class TW>
+DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const C2 *tws, int t,
                          uint32_t *accA, uint32_t *accB) {
     C2 e[2][8];
 #pragma unroll
@@ -291,36 +394,47 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const LaneTw &T, co
         e[0][q] = fa[br3(q)];
         e[1][q] = fb[br3(q)];
     }
-    fft512<2, true>(e, xb, T, t);
+    fft512_x2<true>(e, xb, T, t);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         double ra, ia, rb, ib;
-        untwist_out(e[0][q], twl[q], ra, ia);
-        untwist_out(e[1][q], twl[q], rb, ib);
-        accA[q] += torus_from_f64(ra);
-        accA[q + 8] += torus_from_f64(ia);
-        accB[q] += torus_from_f64(rb);
-        accB[q + 8] += torus_from_f64(ib);
+        const C2 w = tws[q * TS];
+        untwist_out(e[0][q], w, ra, ia);
+        untwist_out(e[1][q], w, rb, ib);
+        accA[q] += to_torus<SMALL>(ra);
+        accA[q + 8] += to_torus<SMALL>(ia);
+        accB[q] += to_torus<SMALL>(rb);
+        accB[q + 8] += to_torus<SMALL>(ib);
     }
+}
+
+// Forward transforms + MAC of row pair (2RP, 2RP+1) against `bk` (the pair's
+// two TRGSW rows in device layout, global or LDS).
+template <int L, int RP, int TS, class TW>
+DEV void forward_pair(const uint32_t *tA, const uint32_t *tB, int bgbit, const TW &T, const C2 *tws,
+                      C2 *xb, int t, C2 (*d)[8]) {
+    load_digits<L, 2 * RP, TS>(d[0], tA, tB, bgbit, tws);
+    load_digits<L, 2 * RP + 1, TS>(d[1], tA, tB, bgbit, tws);
+    fft512_x2<false>(d, xb, T, t);
+}
+
+template <int RP>
+DEV void mac_pair(C2 *fa, C2 *fb, C2 (*d)[8], const double2 *bk, int t) {
+    mac_row<RP == 0>(fa, fb, d[0], bk, t);
+    mac_row<false>(fa, fb, d[1], bk + 1024, t);
 }
 
 // ExternalProduct(BK row, tmp) for one TRLWE with the BK row read from global
 // memory (stage kernel); tmp per lane as (value + offset) at t + 64m.
-template <int L>
-DEV void external_product_add(const uint32_t *tA, const uint32_t *tB, const double2 *__restrict__ bkrow,
-                              int bgbit, const LaneTw &T, const C2 *twl, C2 *xb, int t,
-                              uint32_t *accA, uint32_t *accB) {
-    C2 fa[8], fb[8];
-#pragma unroll 1
-    for (int rp = 0; rp < L; rp++) {
+template <int L, int RP = 0>
+DEV void ext_pairs_global(const uint32_t *tA, const uint32_t *tB, const double2 *__restrict__ bkrow, int bgbit,
+                          const RegTw &T, const C2 *twl, C2 *xb, int t, C2 *fa, C2 *fb) {
+    if constexpr (RP < L) {
         C2 d[2][8];
-        load_digits<L>(d[0], tA, tB, 2 * rp, bgbit, twl);
-        load_digits<L>(d[1], tA, tB, 2 * rp + 1, bgbit, twl);
-        fft512<2, false>(d, xb, T, t);
-        mac_row(fa, fb, d[0], bkrow + (size_t)(2 * rp) * 1024, t, rp == 0);
-        mac_row(fa, fb, d[1], bkrow + (size_t)(2 * rp + 1) * 1024, t, false);
+        forward_pair<L, RP, 1>(tA, tB, bgbit, T, twl, xb, t, d);
+        mac_pair<RP>(fa, fb, d, bkrow + (size_t)RP * 2048, t);
+        ext_pairs_global<L, RP + 1>(tA, tB, bkrow, bgbit, T, twl, xb, t, fa, fb);
     }
-    inverse_and_add(fa, fb, xb, T, twl, t, accA, accB);
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -344,17 +458,60 @@ DEV void issue_bk_pair(const double2 *__restrict__ src, double2 *lds, int tid) {
 // then sampleExtractIndex(acc, 0) (TLWELv1) or the TRLWE itself.
 // The four waves consume the same BK rows, so each row pair is brought into
 // LDS once per block by LDS-DMA, issued right after the previous pair's MAC
-// and landing under the next forward FFTs.  Everything else (accumulator,
-// FFT exchanges) lives in wave-private LDS and needs no block barrier.
+// and landing under the next forward FFTs.  FFT twiddles and twist factors
+// are read from one block-shared LDS copy.  Accumulator and FFT exchanges
+// live in wave-private LDS and need no block barrier.
 // ---------------------------------------------------------------------------
 constexpr int BR_WAVES = 4;
 constexpr int BR_LDS_BK = 2048 * 16;                  // one row pair, double2
+constexpr int BR_LDS_TW = 512 * 16;                   // stage twiddles (511 used)
+constexpr int BR_LDS_TWIST = 512 * 16;                // twist factors
 constexpr int BR_LDS_ACC = 2048 * 4;                  // per wave
 constexpr int BR_LDS_X = 2 * 512 * 16;                // per wave, NF = 2
 constexpr int BR_LDS_AT = 1024 * 2;                   // per wave
-constexpr int BR_LDS_TOTAL = BR_LDS_BK + BR_WAVES * (BR_LDS_ACC + BR_LDS_X + BR_LDS_AT);
+constexpr int BR_LDS_TOTAL =
+    BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST + BR_WAVES * (BR_LDS_ACC + BR_LDS_X + BR_LDS_AT);
 
+// Digits of decomposition row `row` read from the wave's LDS copy of
+// (rot - acc + offset): polynomial a at [0, 1024), b at [1024, 2048).  `row`
+// is a runtime value (rolled pair loop); only pointer and shift depend on it.
+DEV void load_digits_lds(C2 *d, const uint32_t *s_tmp, int row, int L, int bgbit, const C2 *twist_t, int t) {
+    const bool from_a = row < L;
+    const uint32_t *src = s_tmp + (from_a ? 0 : 1024) + t;
+    const int level = from_a ? row : row - L;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int m = br3(q);
+        d[q] = twist_in(digit_f64(src[64 * m], level, bgbit), digit_f64(src[64 * (m + 8)], level, bgbit),
+                        twist_t[64 * m]);
+    }
+}
+
+// Row pairs of one CMUX step: forward FFTs of rows (2rp, 2rp+1), wait for the
+// pair's BK rows in LDS, MAC, release the buffer and prefetch the next pair.
 template <int L>
+DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
+                  C2 *fa, C2 *fb, double2 *s_bk, const double2 *__restrict__ next_pair, bool has_next) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
+        fa[q] = c2(0.0, 0.0);
+        fb[q] = c2(0.0, 0.0);
+    }
+#pragma unroll 1
+    for (int rp = 0; rp < L; rp++) {
+        C2 d[2][8];
+        load_digits_lds(d[0], s_tmp, 2 * rp, L, bgbit, twist_t, t);
+        load_digits_lds(d[1], s_tmp, 2 * rp + 1, L, bgbit, twist_t, t);
+        fft512_x2<false>(d, xb, T, t);
+        __syncthreads();  // BK pair has landed (s_waitcnt vmcnt(0) + s_barrier)
+        mac_row<false>(fa, fb, d[0], s_bk, t);
+        mac_row<false>(fa, fb, d[1], s_bk + 1024, t);
+        __syncthreads();  // every wave is done reading the pair
+        if (rp + 1 < L || has_next) issue_bk_pair(next_pair + (size_t)rp * 2048, s_bk, tid);
+    }
+}
+
+template <int L, bool SMALL>
 __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ testvec,
@@ -365,10 +522,12 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     const int t = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     double2 *s_bk = reinterpret_cast<double2 *>(smem);
-    uint32_t *s_acc = reinterpret_cast<uint32_t *>(smem + BR_LDS_BK + w * BR_LDS_ACC);
-    C2 *s_x = reinterpret_cast<C2 *>(smem + BR_LDS_BK + BR_WAVES * BR_LDS_ACC + w * BR_LDS_X);
-    uint16_t *s_at = reinterpret_cast<uint16_t *>(smem + BR_LDS_BK + BR_WAVES * (BR_LDS_ACC + BR_LDS_X) +
-                                                  w * BR_LDS_AT);
+    C2 *s_tw = reinterpret_cast<C2 *>(smem + BR_LDS_BK);
+    C2 *s_twist = reinterpret_cast<C2 *>(smem + BR_LDS_BK + BR_LDS_TW);
+    unsigned char *wbase = smem + BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;
+    uint32_t *s_acc = reinterpret_cast<uint32_t *>(wbase + w * BR_LDS_ACC);
+    C2 *s_x = reinterpret_cast<C2 *>(wbase + BR_WAVES * BR_LDS_ACC + w * BR_LDS_X);
+    uint16_t *s_at = reinterpret_cast<uint16_t *>(wbase + BR_WAVES * (BR_LDS_ACC + BR_LDS_X) + w * BR_LDS_AT);
 
     const int n = P.n;
     const size_t g_raw = (size_t)blockIdx.x * BR_WAVES + w;
@@ -377,10 +536,11 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     const uint32_t *A = in_a + g * (size_t)(n + 1);
     const uint32_t *Bv = in_b ? in_b + g * (size_t)(n + 1) : A;
     const int op = ops ? (int)ops[g] : 255;
-    const size_t row_pair = 2048;                     // double2 per BK row pair
-    const size_t step_stride = (size_t)L * row_pair;  // double2 per TRGSW (BK[i])
+    const size_t step_stride = (size_t)L * 2048;  // double2 per TRGSW (BK[i])
 
     issue_bk_pair(bkd, s_bk, tid);  // pair (0, 0), lands under the prologue
+    for (int x = tid; x < 511; x += 256) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 256) s_twist[x] = TT.twist[x];
 
     // a~_i = (a_i + 2^20) >> 21 and b~ = 2N - ((b + 2^20) >> 21), 64-bit adds
     // (trgsw.zig:297, :312).
@@ -392,11 +552,6 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         else bt = 2048 - (int)tl;
     }
     bt = __builtin_amdgcn_readlane(bt, n & 63);
-    LaneTw T;
-    load_lane_tw(T, TT.tw, t);
-    C2 twl[8];
-#pragma unroll
-    for (int m = 0; m < 8; m++) twl[m] = TT.twist[t + 64 * m];
 
     // acc = X^{b~} * testvec (trgsw.zig:300-306), lane owns k = t + 64m.
     uint32_t accA[16], accB[16];
@@ -407,33 +562,35 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         s_acc[t + 64 * m] = accA[m];
         s_acc[1024 + t + 64 * m] = accB[m];
     }
-    wave_sync();
+    __syncthreads();  // tables visible to every wave
+    LdsTw T;
+    T.init(s_tw);
+    const C2 *twist_t = s_twist + t;  // twist of coefficient t + 64m at [64m]
 
     for (int i = 0; i < n; i++) {
         // a~ in {0, 2N} gives tmp = 0 and an exactly-zero external product;
         // it is computed anyway so the four waves keep one barrier schedule.
         const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
+        // tmp = X^{a~} acc - acc (+ decomposition offset), written over the
+        // accumulator's LDS copy (the old acc stays in accA/accB registers)
         uint32_t tA[16], tB[16];
 #pragma unroll
         for (int m = 0; m < 16; m++) {
             tA[m] = rot_read(s_acc, t + 64 * m, at) - accA[m] + P.offset;
             tB[m] = rot_read(s_acc + 1024, t + 64 * m, at) - accB[m] + P.offset;
         }
-        C2 fa[8], fb[8];
-#pragma unroll 1
-        for (int rp = 0; rp < L; rp++) {
-            C2 d[2][8];
-            load_digits<L>(d[0], tA, tB, 2 * rp, P.bgbit, twl);
-            load_digits<L>(d[1], tA, tB, 2 * rp + 1, P.bgbit, twl);
-            fft512<2, false>(d, s_x, T, t);
-            __syncthreads();  // BK pair (i, rp) has landed (s_waitcnt vmcnt(0) + s_barrier)
-            mac_row(fa, fb, d[0], s_bk, t, rp == 0);
-            mac_row(fa, fb, d[1], s_bk + 1024, t, false);
-            __syncthreads();  // every wave is done reading the pair
-            const size_t nxt = (size_t)i * step_stride + (size_t)(rp + 1) * row_pair;
-            if (rp + 1 < L || i + 1 < n) issue_bk_pair(bkd + nxt, s_bk, tid);
+        wave_sync();
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            s_acc[t + 64 * m] = tA[m];
+            s_acc[1024 + t + 64 * m] = tB[m];
         }
-        inverse_and_add(fa, fb, s_x, T, twl, t, accA, accB);
+        wave_sync();
+        C2 fa[8], fb[8];
+        br_pairs<L>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, bkd + (size_t)i * step_stride + 2048,
+                    i + 1 < n);
+        inverse_and_add<SMALL, 64>(fa, fb, s_x, T, twist_t, t, accA, accB);
+        wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) {
             s_acc[t + 64 * m] = accA[m];
@@ -592,8 +749,8 @@ __global__ __launch_bounds__(64) void k_fft_forward(DevTables TT, const uint32_t
     __shared__ C2 s_x[512];
     const int t = threadIdx.x;
     const uint32_t *x = in + (size_t)blockIdx.x * 1024;
-    LaneTw T;
-    load_lane_tw(T, TT.tw, t);
+    RegTw T;
+    T.init(TT.tw, t);
     C2 d[1][8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -615,8 +772,8 @@ __global__ __launch_bounds__(64) void k_fft_inverse(DevTables TT, const double *
     __shared__ C2 s_x[512];
     const int t = threadIdx.x;
     const double *f = in + (size_t)blockIdx.x * 1024;
-    LaneTw T;
-    load_lane_tw(T, TT.tw, t);
+    RegTw T;
+    T.init(TT.tw, t);
     C2 d[1][8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -644,8 +801,8 @@ __global__ __launch_bounds__(64) void k_poly_mul(DevTables TT, const uint32_t *_
     const int t = threadIdx.x;
     const uint32_t *x = a + (size_t)blockIdx.x * 1024;
     const uint32_t *y = b + (size_t)blockIdx.x * b_stride;
-    LaneTw T;
-    load_lane_tw(T, TT.tw, t);
+    RegTw T;
+    T.init(TT.tw, t);
     C2 twl[8];
 #pragma unroll
     for (int m = 0; m < 8; m++) twl[m] = TT.twist[t + 64 * m];
@@ -690,8 +847,8 @@ __global__ __launch_bounds__(64) void k_external_product(KParams P, DevTables TT
     __shared__ C2 s_x[2 * 512];
     const int t = threadIdx.x;
     const uint32_t *x = in + (size_t)blockIdx.x * 2048;
-    LaneTw T;
-    load_lane_tw(T, TT.tw, t);
+    RegTw T;
+    T.init(TT.tw, t);
     C2 twl[8];
 #pragma unroll
     for (int m = 0; m < 8; m++) twl[m] = TT.twist[t + 64 * m];
@@ -703,7 +860,9 @@ __global__ __launch_bounds__(64) void k_external_product(KParams P, DevTables TT
         accA[m] = 0;
         accB[m] = 0;
     }
-    external_product_add<L>(tA, tB, bkrow, P.bgbit, T, twl, s_x, t, accA, accB);
+    C2 fa[8], fb[8];
+    ext_pairs_global<L>(tA, tB, bkrow, P.bgbit, T, twl, s_x, t, fa, fb);
+    inverse_and_add<false, 1>(fa, fb, s_x, T, twl, t, accA, accB);
     uint32_t *o = out + (size_t)blockIdx.x * 2048;
 #pragma unroll
     for (int m = 0; m < 16; m++) {
@@ -747,22 +906,19 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     if (B == 0) return hipSuccess;
     dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(64 * BR_WAVES);
     const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
+    // |external product| <= 2L * N * Bg/2 * 2^31: the 8-op exact conversion
+    // needs it below 2^51 (true for the L=3 / Bg=2^6 sets, false for UINT4)
+    const bool small = std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 50);
+#define BR_LAUNCH(L_, S_)                                                                                    \
+    hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out, \
+                       out_mode, B)
     switch (P.L) {
-    case 1:
-        hipLaunchKernelGGL(k_blind_rotate<1>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out,
-                           out_mode, B);
-        break;
-    case 2:
-        hipLaunchKernelGGL(k_blind_rotate<2>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out,
-                           out_mode, B);
-        break;
-    case 3:
-        hipLaunchKernelGGL(k_blind_rotate<3>, grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out,
-                           out_mode, B);
-        break;
-    default:
-        return hipErrorInvalidValue;
+    case 1: if (small) BR_LAUNCH(1, true); else BR_LAUNCH(1, false); break;
+    case 2: if (small) BR_LAUNCH(2, true); else BR_LAUNCH(2, false); break;
+    case 3: if (small) BR_LAUNCH(3, true); else BR_LAUNCH(3, false); break;
+    default: return hipErrorInvalidValue;
     }
+#undef BR_LAUNCH
     return hipGetLastError();
 }
 
