@@ -90,12 +90,19 @@ def test_key_switch_vs_oracle(oracle, pname, B):
 
 
 # ---- blind rotation / bootstrap ---------------------------------------------
+@pytest.mark.parametrize("form", ["whole", "split"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
-def test_blind_rotate_vs_oracle(oracle, pname, B):
+def test_blind_rotate_vs_oracle(oracle, pname, B, form, monkeypatch):
+    """Both kernel forms (1 wave per item / 2 waves per item) bit-exact."""
+    monkeypatch.setenv("TFHE_BR_KERNEL", form)
     c, k = ctx_for(oracle, pname)
     cts = u32rand(rng(6), B, k.p.n + 1)  # uniform TLWE: bit-exactness only
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
     assert np.array_equal(c.blind_rotate_batch(cts), want)
+    # odd batch sizes leave idle item slots in the last workgroup
+    cts5 = u32rand(rng(16), 5, k.p.n + 1)
+    want5 = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts5])
+    assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
 def test_gate_golden_vectors(oracle):

@@ -617,6 +617,173 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
 }
 
 // ---------------------------------------------------------------------------
+// Blind rotation, split form: TWO wavefronts per item, 4 items per 512-thread
+// block (2 waves per SIMD).  Wave h of an item owns accumulator polynomial h
+// (h = 0: a, 1: b) for the tmp / inverse / update phases.  The 2L decomposed
+// rows are dealt out interleaved: in round r wave h forward-transforms row
+// 2r + h (polynomial (2r+h)/L, level (2r+h)%L; it reads the partner's tmp from
+// LDS when the row belongs to the other polynomial) and publishes the spectrum.
+// Round r thus holds rows 2r and 2r+1 — consecutive — so every wave adds both
+// terms to its output polynomial in the reference's row order 0..2L-1 with no
+// terms held across rounds.  Finally each wave inverse-transforms its own
+// output and updates its own polynomial.
+// ---------------------------------------------------------------------------
+constexpr int BS_GATES = 4;
+constexpr int BS_WAVES = 2 * BS_GATES;
+constexpr int BS_LDS_BK = 2 * 1024 * 16;   // rows 2r and 2r+1, double2
+constexpr int BS_LDS_TW = 512 * 16;
+constexpr int BS_LDS_TWIST = 512 * 16;
+constexpr int BS_LDS_ACC = 1024 * 4;       // per wave: its polynomial (then its digits' source)
+constexpr int BS_LDS_X = 512 * 16;         // per wave: FFT exchanges, then its spectrum
+constexpr int BS_LDS_AT = 1024 * 2;        // per item
+constexpr int BS_LDS_TOTAL =
+    BS_LDS_BK + BS_LDS_TW + BS_LDS_TWIST + BS_WAVES * (BS_LDS_ACC + BS_LDS_X) + BS_GATES * BS_LDS_AT + 64;
+
+// LDS-DMA of rows (2r, 2r+1) of BK[i] (contiguous 32 KB): 512 threads x 4.
+DEV void issue_bk_rows(const double2 *__restrict__ rows, double2 *lds, int tid) {
+    const int wbase = tid & ~63;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+        __builtin_amdgcn_global_load_lds((global_void_t *)(rows + 512 * c + tid),
+                                         (lds_void_t *)(lds + 512 * c + wbase), 16, 0, 0);
+}
+
+// term = D * BK row part (fmaInFd1024's (a_re*b_re - a_im*b_im, a_re*b_im + a_im*b_re))
+DEV C2 cmul_bk(C2 d, double2 k) { return c2(d.x * k.x - d.y * k.y, d.x * k.y + d.y * k.x); }
+
+template <int L, bool SMALL>
+__global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
+    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ testvec,
+    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[BS_LDS_TOTAL];
+    const int tid = threadIdx.x;
+    const int t = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gs = w >> 1;  // item slot in the block
+    const int h = w & 1;    // polynomial owned by this wave
+    double2 *s_bk = reinterpret_cast<double2 *>(smem);
+    C2 *s_tw = reinterpret_cast<C2 *>(smem + BS_LDS_BK);
+    C2 *s_twist = reinterpret_cast<C2 *>(smem + BS_LDS_BK + BS_LDS_TW);
+    unsigned char *base = smem + BS_LDS_BK + BS_LDS_TW + BS_LDS_TWIST;
+    uint32_t *s_acc = reinterpret_cast<uint32_t *>(base + w * BS_LDS_ACC);
+    C2 *s_xg = reinterpret_cast<C2 *>(base + BS_WAVES * BS_LDS_ACC + (2 * gs) * BS_LDS_X);  // item's pair
+    C2 *s_x = s_xg + h * 512;
+    uint16_t *s_at = reinterpret_cast<uint16_t *>(base + BS_WAVES * (BS_LDS_ACC + BS_LDS_X) + gs * BS_LDS_AT);
+    int *s_bt = reinterpret_cast<int *>(base + BS_WAVES * (BS_LDS_ACC + BS_LDS_X) + BS_GATES * BS_LDS_AT);
+
+    const int n = P.n;
+    const size_t g_raw = (size_t)blockIdx.x * BS_GATES + gs;
+    const bool valid = g_raw < B;
+    const size_t g = valid ? g_raw : B - 1;
+    const uint32_t *A = in_a + g * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + g * (size_t)(n + 1) : A;
+    const int op = ops ? (int)ops[g] : 255;
+    const size_t trgsw = (size_t)2 * L * 1024;  // double2 per BK[i]
+
+    issue_bk_rows(bkd, s_bk, tid);  // step 0, round 0
+    for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
+    if (h == 0) {
+        for (int i = t; i <= n; i += 64) {
+            uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
+            uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
+            if (i < n) s_at[i] = (uint16_t)tl;
+            else s_bt[gs] = 2048 - (int)tl;
+        }
+    }
+    __syncthreads();
+    const int bt = __builtin_amdgcn_readfirstlane(s_bt[gs]);
+    const uint32_t *tv = testvec + h * 1024;
+    uint32_t acc[16];  // own polynomial at coefficients t + 64m
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        acc[m] = rot_read(tv, t + 64 * m, bt);
+        s_acc[t + 64 * m] = acc[m];
+    }
+    LdsTw T;
+    T.init(s_tw);
+    const C2 *twist_t = s_twist + t;
+    const C2 *spec_0 = s_xg;        // spectrum of row 2r (wave 0 of the item)
+    const C2 *spec_1 = s_xg + 512;  // spectrum of row 2r+1 (wave 1)
+    const uint32_t *s_tmp_item = reinterpret_cast<const uint32_t *>(base + (2 * gs) * BS_LDS_ACC);
+    wave_sync();
+
+    for (int i = 0; i < n; i++) {
+        const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
+        // own tmp = X^{a~} p - p + offset, staged over the polynomial's LDS copy
+        uint32_t tm[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++) tm[m] = rot_read(s_acc, t + 64 * m, at) - acc[m] + P.offset;
+        wave_sync();
+#pragma unroll
+        for (int m = 0; m < 16; m++) s_acc[t + 64 * m] = tm[m];
+        __syncthreads();  // both tmps visible to both waves of the item
+        C2 S[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) S[q] = c2(0.0, 0.0);  // the reference's zeroed accumulator
+#pragma unroll 1
+        for (int r = 0; r < L; r++) {
+            const int row = 2 * r + h;
+            const int poly = row >= L ? 1 : 0;
+            const int level = row - poly * L;
+            C2 d[1][8];
+            const uint32_t *src = s_tmp_item + poly * 1024 + t;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int m = br3(q);
+                d[0][q] = twist_in(digit_f64(src[64 * m], level, P.bgbit),
+                                   digit_f64(src[64 * (m + 8)], level, P.bgbit), twist_t[64 * m]);
+            }
+            fft512<1, false>(d, s_x, T, t);
+#pragma unroll
+            for (int q = 0; q < 8; q++) s_x[t + 64 * q] = d[0][q];  // publish this row's spectrum
+            __syncthreads();  // spectra of rows 2r, 2r+1 and BK rows 2r, 2r+1 are in LDS
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const C2 t0 = cmul_bk(spec_0[t + 64 * q], s_bk[(2 * q + h) * 64 + t]);
+                const C2 t1 = cmul_bk(spec_1[t + 64 * q], s_bk[1024 + (2 * q + h) * 64 + t]);
+                S[q] = c2(S[q].x + t0.x, S[q].y + t0.y);
+                S[q] = c2(S[q].x + t1.x, S[q].y + t1.y);
+            }
+            __syncthreads();  // spectra and BK rows consumed
+            if (r + 1 < L) issue_bk_rows(bkd + (size_t)i * trgsw + (size_t)(2 * r + 2) * 1024, s_bk, tid);
+            else if (i + 1 < n) issue_bk_rows(bkd + (size_t)(i + 1) * trgsw, s_bk, tid);
+        }
+        // inverse transform of the own output polynomial, acc' = ExtProd + acc
+        C2 e[1][8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) e[0][q] = S[br3(q)];
+        fft512<1, true>(e, s_x, T, t);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            double re, im;
+            untwist_out(e[0][q], twist_t[64 * q], re, im);
+            acc[q] += to_torus<SMALL>(re);
+            acc[q + 8] += to_torus<SMALL>(im);
+        }
+        wave_sync();
+#pragma unroll
+        for (int m = 0; m < 16; m++) s_acc[t + 64 * m] = acc[m];
+        wave_sync();
+    }
+
+    if (!valid) return;
+    if (out_mode == BR_OUT_LV1) {
+        // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
+        uint32_t *o = out + g * (size_t)1025;
+        if (h == 0) {
+            for (int j = t; j < 1024; j += 64) o[j] = j == 0 ? s_acc[0] : 0u - s_acc[1024 - j];
+        } else if (t == 0) {
+            o[1024] = s_acc[0];
+        }
+    } else {
+        uint32_t *o = out + g * (size_t)2048 + h * 1024;
+        for (int j = t; j < 1024; j += 64) o[j] = s_acc[j];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Identity key switching (trgsw.zig:471-502):
 //   res = (0,...,0, b) - sum_{i<N, j<t} KSK[i][j][digit_j(a_i + 2^(32-(1+basebit*t)))]
 // Integer gather-subtract; the k = 0 rows of the device KSK are zero (the
@@ -904,14 +1071,31 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
                                const double *bkd, uint32_t *out, int out_mode, size_t B,
                                hipStream_t s) {
     if (B == 0) return hipSuccess;
-    dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(64 * BR_WAVES);
     const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
     // |external product| <= 2L * N * Bg/2 * 2^31: the 8-op exact conversion
     // needs it below 2^51 (true for the L=3 / Bg=2^6 sets, false for UINT4)
     const bool small = std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 50);
-#define BR_LAUNCH(L_, S_)                                                                                    \
-    hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2, out, \
-                       out_mode, B)
+    // kernel form: whole (1 wave per item, default: measured faster) or split
+    // (2 waves per item); knob TFHE_BR_KERNEL=whole|split for A/B runs and tests
+    const char *form = getenv("TFHE_BR_KERNEL");
+    const bool split = form && form[0] == 's';
+    dim3 grid, block;
+    if (split) {
+        grid = dim3((unsigned)((B + BS_GATES - 1) / BS_GATES));
+        block = dim3(64 * BS_WAVES);
+    } else {
+        grid = dim3((unsigned)((B + BR_WAVES - 1) / BR_WAVES));
+        block = dim3(64 * BR_WAVES);
+    }
+#define BR_LAUNCH(L_, S_)                                                                                         \
+    do {                                                                                                          \
+        if (split)                                                                                                \
+            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, testvec, \
+                               bk2, out, out_mode, B);                                                            \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2,  \
+                               out, out_mode, B);                                                                 \
+    } while (0)
     switch (P.L) {
     case 1: if (small) BR_LAUNCH(1, true); else BR_LAUNCH(1, false); break;
     case 2: if (small) BR_LAUNCH(2, true); else BR_LAUNCH(2, false); break;
