@@ -37,6 +37,24 @@ def algorithmic_bytes_per_gate(p) -> int:
     return p.n * 2 * p.L * 2 * p.N * 8 + 2 * (p.n + 1) * 4 + (p.N + 1) * 4
 
 
+def f64_ops_per_cmux(L: int) -> int:
+    """Algorithmic f64 adds+muls of one CMUX (no FMA: the reference's
+    expression trees), excluding torus conversion: 2L forward + 2 inverse
+    512-point radix-2 FFTs (1,793 non-trivial butterflies x 4 mul + 2 add,
+    2,304 x 4 add), 2L twists + 2 untwists (4 mul + 2 add per point, + the
+    1/1024 norm), 2L x 2 x 512 complex MACs (4 mul + 4 add).  L=3: 235,568;
+    matches SQ_INSTS_VALU_{ADD,MUL}_F64 x 64 to within the conversion adds
+    (profiles/r01_pmc_blind_rotate_whole.txt)."""
+    fft_mul, fft_add = 1793 * 4, 1793 * 2 + 2304 * 4
+    fwd, inv = 2 * L, 2
+    mul = (fwd + inv) * fft_mul + fwd * 2048 + inv * (2048 + 1024) + 2 * L * 2 * 512 * 4
+    add = (fwd + inv) * fft_add + fwd * 1024 + inv * 1024 + 2 * L * 2 * 512 * 4
+    return mul + add
+
+
+VALU_F64_PEAK = 256 * 4 * 16 * 2.4e9  # non-FMA f64 ops/s: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz (78.6 TF FMA spec / 2)
+
+
 def cpu_baseline(p, sk, bk, ksk, A, B, gpu_out, seconds: float):
     """Oracle (C restatement of zig-tfhe's CPU path, -O3) on the host cores,
     on a bounded sample of the same workload; also spot-checks GPU bits."""
@@ -150,6 +168,8 @@ def main():
         ks_avg_s = ks_ms / 1e3 / max(1, launches)
         alg = algorithmic_bytes_per_gate(p) * B
         achieved = alg / br_avg_s
+        f64_rate = f64_ops_per_cmux(p.L) * p.n * B / br_avg_s
+        form = "split" if os.environ.get("TFHE_BR_KERNEL", "").startswith("s") else "whole"
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_blind_rotate_r01.json")
         if os.path.exists(pmc_path):
@@ -166,8 +186,10 @@ def main():
                        "global_batch": B * world, "params": args.params, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK_BPS / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_BPS, 4), "traffic": traffic,
-                         "kernel": "k_blind_rotate<3>", "kernel_avg_ms": round(br_avg_s * 1e3, 3),
+                         "kernel": f"k_blind_rotate<{p.L}> ({form} form)", "kernel_avg_ms": round(br_avg_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": alg},
+            "valu_f64": {"achieved": round(f64_rate / 1e12, 2), "peak": round(VALU_F64_PEAK / 1e12, 1),
+                         "unit": "Tops/s (f64 add+mul, no FMA)", "frac": round(f64_rate / VALU_F64_PEAK, 4)},
             "key_switch_avg_ms": round(ks_avg_s * 1e3, 3),
             "decrypt_check": all_correct,
         }

@@ -102,6 +102,11 @@ int tfhe_gpu_import_key_device(tfhe_gpu_ctx *ctx, const void *bsk_dev, const voi
 /* ---- Bootstrap / gates (host buffers, synchronous) ---------------------- */
 /* VanillaBootstrap.bootstrap (vanilla.zig:38-52) over B TLWELv0. */
 int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, uint32_t *out, size_t B);
+/* VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69): blind
+ * rotation + sampleExtractIndex2(acc, 0) (trlwe.zig:165-180), n+1 words per
+ * item in the reference's hybrid form (p[0]=a[0], p[i]=-a[n-i], p[n]=b[0]). */
+int tfhe_gpu_bootstrap_without_key_switch_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, uint32_t *out,
+                                                size_t B);
 /* Gates.*Gate (gates.zig:48-121): per-item op + pre-combination + bootstrap. */
 int tfhe_gpu_gate_batch(tfhe_gpu_ctx *ctx, const uint8_t *ops, const uint32_t *a,
                         const uint32_t *b, uint32_t *out, size_t B);

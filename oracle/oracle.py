@@ -161,6 +161,20 @@ class Oracle:
         self.lib.oracle_sample_extract_index(C.c_uint32(N), _ptr(trlwe, u32p), C.c_uint32(k), _ptr(out, u32p))
         return out
 
+    def sample_extract_index2(self, p, trlwe, k):
+        trlwe = np.ascontiguousarray(trlwe, dtype=np.uint32)
+        out = np.zeros(p.n + 1, dtype=np.uint32)
+        self.lib.oracle_sample_extract_index2(C.c_uint32(p.n), C.c_uint32(p.N), _ptr(trlwe, u32p), C.c_uint32(k),
+                                              _ptr(out, u32p))
+        return out
+
+    def bootstrap_without_key_switch(self, p, tlwe, keys):
+        tlwe = np.ascontiguousarray(tlwe, dtype=np.uint32)
+        out = np.zeros(p.n + 1, dtype=np.uint32)
+        self.lib.oracle_bootstrap_without_key_switch(C.byref(p), _ptr(tlwe, u32p), _ptr(keys.testvec, u32p),
+                                                     _ptr(keys.bk, f64p), C.c_uint32(keys.offset), _ptr(out, u32p))
+        return out
+
     def identity_key_switch(self, p, lv1, ksk):
         lv1 = np.ascontiguousarray(lv1, dtype=np.uint32)
         out = np.zeros(p.n + 1, dtype=np.uint32)

@@ -409,6 +409,17 @@ void oracle_sample_extract_index(uint32_t N, const uint32_t *trlwe, uint32_t k, 
     out[N] = trlwe[N + k];
 }
 
+/* sampleExtractIndex2 — trlwe.zig:165-180.  The reference bounds the loop
+ * by tlwe_lv0.N (= n), not the ring size: p[i] = a[k-i] (i<=k),
+ * -a[n+k-i] (k<i<n), p[n] = b[k] (b at offset N in the TRLWE). */
+void oracle_sample_extract_index2(uint32_t n, uint32_t N, const uint32_t *trlwe, uint32_t k, uint32_t *out) {
+    for (uint32_t i = 0; i < n; i++) {
+        if (i <= k) out[i] = trlwe[k - i];
+        else out[i] = 0u - trlwe[n + k - i];
+    }
+    out[n] = trlwe[N + k];
+}
+
 /* identityKeySwitching — trgsw.zig:471-502; ksk layout [(BASE*T*i)+(BASE*j)+k][n+1] */
 void oracle_identity_key_switch(const oracle_params *p, const uint32_t *src, const uint32_t *ksk,
                                 uint32_t *res) {
@@ -440,6 +451,15 @@ void oracle_bootstrap(const oracle_params *p, const uint32_t *in, const uint32_t
     oracle_sample_extract_index(N, acc, 0, lv1);
     oracle_identity_key_switch(p, lv1, ksk, out);
     free(acc); free(lv1);
+}
+
+/* VanillaBootstrap.bootstrapWithoutKeySwitch — vanilla.zig:58-69 */
+void oracle_bootstrap_without_key_switch(const oracle_params *p, const uint32_t *in, const uint32_t *testvec,
+                                         const double *bk, uint32_t offset, uint32_t *out) {
+    uint32_t *acc = (uint32_t *)malloc(sizeof(uint32_t) * 2 * p->N);
+    oracle_blind_rotate(p, in, testvec, bk, offset, acc);
+    oracle_sample_extract_index2(p->n, p->N, acc, 0, out);
+    free(acc);
 }
 
 /* Gate linear pre-combination — gates.zig:48-121 (tlwe.zig:120-239 ops),

@@ -74,12 +74,17 @@ void oracle_blind_rotate(const oracle_params *p, const uint32_t *tlwe_lv0 /*n+1*
                          const uint32_t *testvec /*2N*/, const double *bk, uint32_t offset,
                          uint32_t *out /*2N*/);
 void oracle_sample_extract_index(uint32_t N, const uint32_t *trlwe, uint32_t k, uint32_t *out /*N+1*/);
+void oracle_sample_extract_index2(uint32_t n, uint32_t N, const uint32_t *trlwe, uint32_t k,
+                                  uint32_t *out /*n+1*/);
 void oracle_identity_key_switch(const oracle_params *p, const uint32_t *tlwe_lv1 /*N+1*/,
                                 const uint32_t *ksk, uint32_t *out /*n+1*/);
 
 /* ---- bootstrap / gates (bootstrap/vanilla.zig, gates.zig) */
 void oracle_bootstrap(const oracle_params *p, const uint32_t *in /*n+1*/, const uint32_t *testvec,
                       const double *bk, const uint32_t *ksk, uint32_t offset, uint32_t *out /*n+1*/);
+void oracle_bootstrap_without_key_switch(const oracle_params *p, const uint32_t *in /*n+1*/,
+                                         const uint32_t *testvec, const double *bk, uint32_t offset,
+                                         uint32_t *out /*n+1*/);
 /* op codes: see include/tfhe_gpu.h TFHE_GATE_* (same numbering) */
 void oracle_gate_combine(const oracle_params *p, int op, const uint32_t *a, const uint32_t *b,
                          uint32_t *out /*n+1*/);

@@ -105,6 +105,21 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form, monkeypatch):
     assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
+@pytest.mark.parametrize("form", ["whole", "split"])
+def test_bootstrap_without_key_switch(oracle, form, monkeypatch):
+    """VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69) and the
+    strategy mirror: blind rotation + the hybrid sampleExtractIndex2."""
+    monkeypatch.setenv("TFHE_BR_KERNEL", form)
+    c, k = ctx_for(oracle, "80")
+    cts = u32rand(rng(26), 3, k.p.n + 1)
+    want = np.array([oracle.bootstrap_without_key_switch(k.p, t, k.ck) for t in cts])
+    assert np.array_equal(c.bootstrap_without_key_switch_batch(cts), want)
+    bs = tfhe_amd.HipBootstrap(c)
+    assert np.array_equal(bs.bootstrap_without_key_switch(cts[0]), want[0])
+    assert np.array_equal(bs.bootstrap(cts[1]), oracle.bootstrap(k.p, cts[1], k.ck))
+    assert bs.name() == "mi355x"
+
+
 def test_gate_golden_vectors(oracle):
     """All ten reference gates, committed inputs/outputs (80-bit, seeds 42/43)."""
     c, _ = ctx_for(oracle, "80")

@@ -174,6 +174,19 @@ def test_sample_extract_deterministic(oracle):  # trlwe.zig:296-318
         assert oracle.sample_extract_index(t, k)[1024] == t[1024 + k]
 
 
+def test_sample_extract_index2_hybrid_form(oracle, keys128):
+    """trlwe.zig:165-180 bounds its loop by tlwe_lv0.N (= n, not the ring
+    size): p[0] = a[0], p[i] = -a[n-i] for 0 < i < n, p[n] = b[0] (k = 0)."""
+    p = keys128.p
+    t = rng(4).integers(0, 2**32, 2048, dtype=np.uint64).astype(np.uint32)
+    got = oracle.sample_extract_index2(p, t, 0)
+    want = np.empty(p.n + 1, np.uint32)
+    want[0] = t[0]
+    want[1:p.n] = (0 - t[p.n - np.arange(1, p.n)].astype(np.int64)) & 0xFFFFFFFF
+    want[p.n] = t[1024]
+    assert np.array_equal(got, want)
+
+
 def test_trlwe_encrypt_decrypt(oracle, keys128):  # trlwe.zig:184-231
     p = keys128.p
     g = rng(3)

@@ -118,9 +118,18 @@ int set_key_common(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv_a, const
     return TFHE_OK;
 }
 
-// Blind rotation (+ optional key switch) over device buffers, async.
+// What a blind-rotation launch hands back.
+enum RunKind : int {
+    RUN_BOOTSTRAP = 0,     // sample extract + key switch: TLWELv0 (vanilla.zig:38-52)
+    RUN_TRLWE = 1,         // the accumulator: TRLWELv1 (trgsw.zig:290-333)
+    RUN_NO_KEYSWITCH = 2,  // sampleExtractIndex2, n+1 words (vanilla.zig:58-69)
+};
+
+// Blind rotation (+ key switch for RUN_BOOTSTRAP) over device buffers, async.
 int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b,
-                      const uint32_t *testvec_dev, uint32_t *out, size_t B, bool key_switch) {
+                      const uint32_t *testvec_dev, uint32_t *out, size_t B, int kind) {
+    const bool key_switch = kind == RUN_BOOTSTRAP;
+    const int out_mode = kind == RUN_BOOTSTRAP ? BR_OUT_LV1 : kind == RUN_TRLWE ? BR_OUT_TRLWE : BR_OUT_LV0_EXTRACT2;
     if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
     if (B == 0) return TFHE_OK;
     int rc = ensure(c, c->s_lv1, B * 1025 * sizeof(uint32_t));
@@ -138,7 +147,7 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
         HIPCHK(c, hipEventRecord(ev[0], c->stream));
     }
     HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
-                                  lv1, key_switch ? BR_OUT_LV1 : BR_OUT_TRLWE, B, c->stream));
+                                  lv1, out_mode, B, c->stream));
     if (ev[1]) HIPCHK(c, hipEventRecord(ev[1], c->stream));
     if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream));
     if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], c->stream));
@@ -416,7 +425,19 @@ int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out,
     const size_t w = tlwe0_words(c);
     int rc = h2d(c, c->s_a, in, B * w * 4);
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
-    if (!rc) rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, nullptr, (uint32_t *)c->s_out.p, B, true);
+    if (!rc) rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, nullptr, (uint32_t *)c->s_out.p, B, RUN_BOOTSTRAP);
+    if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
+    return rc;
+}
+
+int tfhe_gpu_bootstrap_without_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
+    if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = h2d(c, c->s_a, in, B * w * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * w * 4);
+    if (!rc) rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, nullptr, (uint32_t *)c->s_out.p, B, RUN_NO_KEYSWITCH);
     if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
     return rc;
 }
@@ -435,7 +456,7 @@ int tfhe_gpu_gate_batch(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, 
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
     if (!rc)
         rc = run_bootstrap_dev(c, (const uint8_t *)c->s_ops.p, (const uint32_t *)c->s_a.p, (const uint32_t *)c->s_b.p,
-                               nullptr, (uint32_t *)c->s_out.p, B, true);
+                               nullptr, (uint32_t *)c->s_out.p, B, RUN_BOOTSTRAP);
     if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
     return rc;
 }
@@ -453,7 +474,7 @@ int tfhe_gpu_blind_rotate_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint3
         tv = (const uint32_t *)c->s_tv.p;
     }
     if (!rc) rc = ensure(c, c->s_out, B * 2 * c->P.N * 4);
-    if (!rc) rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, tv, (uint32_t *)c->s_out.p, B, false);
+    if (!rc) rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, tv, (uint32_t *)c->s_out.p, B, RUN_TRLWE);
     if (!rc) rc = d2h_sync(c, trlwe_out, c->s_out.p, B * 2 * c->P.N * 4);
     return rc;
 }
@@ -469,7 +490,7 @@ int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
     if (!rc)
         rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, (const uint32_t *)c->s_tv.p,
-                               (uint32_t *)c->s_out.p, B, true);
+                               (uint32_t *)c->s_out.p, B, RUN_BOOTSTRAP);
     if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
     return rc;
 }
@@ -478,13 +499,13 @@ int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *c, const uint8_t *ops_dev, const uint3
                             uint32_t *out_dev, size_t B) {
     if (!c || (B && (!ops_dev || !a_dev || !b_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
     HIPCHK(c, hipSetDevice(c->device));
-    return run_bootstrap_dev(c, ops_dev, a_dev, b_dev, nullptr, out_dev, B, true);
+    return run_bootstrap_dev(c, ops_dev, a_dev, b_dev, nullptr, out_dev, B, RUN_BOOTSTRAP);
 }
 
 int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *c, const uint32_t *in_dev, uint32_t *out_dev, size_t B) {
     if (!c || (B && (!in_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
     HIPCHK(c, hipSetDevice(c->device));
-    return run_bootstrap_dev(c, nullptr, in_dev, nullptr, nullptr, out_dev, B, true);
+    return run_bootstrap_dev(c, nullptr, in_dev, nullptr, nullptr, out_dev, B, RUN_BOOTSTRAP);
 }
 
 int tfhe_gpu_profile_begin(tfhe_gpu_ctx *c) {

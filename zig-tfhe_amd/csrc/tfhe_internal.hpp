@@ -28,6 +28,9 @@ struct KParams {
 enum BrOut : int {
     BR_OUT_LV1 = 0,    // sampleExtractIndex(acc, 0): TLWELv1, N+1 words per item
     BR_OUT_TRLWE = 1,  // the accumulator itself: TRLWELv1, 2N words per item
+    // sampleExtractIndex2(acc, 0) (trlwe.zig:165-180), n+1 words per item: the
+    // reference loops i < tlwe_lv0.N, so p[0] = a[0], p[i] = -a[n-i] (0<i<n), p[n] = b[0]
+    BR_OUT_LV0_EXTRACT2 = 2,
 };
 
 // Device constant tables uploaded once per context (host_tables in tfhe_gpu.cpp).

@@ -610,6 +610,10 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
             else v = s_acc[1024];
             o[j] = v;
         }
+    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {
+        // sampleExtractIndex2(acc, 0) over the lv0 length n (trlwe.zig:165-180)
+        uint32_t *o = out + g * (size_t)(n + 1);
+        for (int j = t; j <= n; j += 64) o[j] = j == 0 ? s_acc[0] : j < n ? 0u - s_acc[n - j] : s_acc[1024];
     } else {
         uint32_t *o = out + g * (size_t)2048;
         for (int j = t; j < 2048; j += 64) o[j] = s_acc[j];
@@ -776,6 +780,14 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
             for (int j = t; j < 1024; j += 64) o[j] = j == 0 ? s_acc[0] : 0u - s_acc[1024 - j];
         } else if (t == 0) {
             o[1024] = s_acc[0];
+        }
+    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {
+        // sampleExtractIndex2(acc, 0) over the lv0 length n (trlwe.zig:165-180)
+        uint32_t *o = out + g * (size_t)(n + 1);
+        if (h == 0) {
+            for (int j = t; j < n; j += 64) o[j] = j == 0 ? s_acc[0] : 0u - s_acc[n - j];
+        } else if (t == 0) {
+            o[n] = s_acc[0];
         }
     } else {
         uint32_t *o = out + g * (size_t)2048 + h * 1024;

@@ -77,6 +77,7 @@ _SIGS = {
     "tfhe_gpu_export_key_device": (C.c_int, [vp, vp, vp, u32p, u32p]),
     "tfhe_gpu_import_key_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p]),
     "tfhe_gpu_bootstrap_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_bootstrap_without_key_switch_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_gate_batch": (C.c_int, [vp, u8p, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_blind_rotate_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_bootstrap_lut_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
@@ -234,6 +235,16 @@ class Context:
                    "bootstrap_batch")
         return out
 
+    def bootstrap_without_key_switch_batch(self, cts):
+        """VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69): the
+        reference's hybrid sampleExtractIndex2 form, n+1 words per item."""
+        cts, cp = _u32(cts)
+        out = np.zeros_like(cts)
+        self.check(self.lib.tfhe_gpu_bootstrap_without_key_switch_batch(self.h, cp, out.ctypes.data_as(u32p),
+                                                                        cts.shape[0]),
+                   "bootstrap_without_key_switch_batch")
+        return out
+
     def gate_batch(self, ops, a, b):
         ops = np.ascontiguousarray(ops, dtype=np.uint8)
         a, ap = _u32(a)
@@ -367,6 +378,31 @@ def lut_generate(params: TfheParams, m: int, f) -> np.ndarray:
     if rc:
         raise TfheError(f"lut_generate: {rc}")
     return tv
+
+
+class HipBootstrap:
+    """The bootstrap strategy object (bootstrap.zig:30-47, vanilla.zig:24-76)
+    on the MI355X: bootstrap / bootstrap_without_key_switch / name, each over a
+    single TLWELv0 (n+1,) or a batch (B, n+1).  The cloud key is the one the
+    Context holds (the reference passes it per call)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    @staticmethod
+    def _run(fn, ct):
+        ct = np.asarray(ct, np.uint32)
+        out = fn(np.atleast_2d(ct))
+        return out[0] if ct.ndim == 1 else out
+
+    def bootstrap(self, ct):  # vanilla.zig:38-52
+        return self._run(self.ctx.bootstrap_batch, ct)
+
+    def bootstrap_without_key_switch(self, ct):  # vanilla.zig:58-69
+        return self._run(self.ctx.bootstrap_without_key_switch_batch, ct)
+
+    def name(self) -> str:  # vanilla.zig:72-75
+        return "mi355x"
 
 
 class Gates:

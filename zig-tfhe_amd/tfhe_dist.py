@@ -19,10 +19,22 @@ def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def _sync(device):
+    import torch
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+
+
 def broadcast_cloud_key(ctx, device, src: int = 0, group=None):
-    """Rank `src` exports its device-resident key blob, every rank receives it
-    by torch.distributed.broadcast (RCCL over xGMI for the nccl backend) and
-    imports it.  Returns the number of bytes broadcast."""
+    """Rank `src` exports its device-resident key blob (BK in the device
+    layout, KSK, decomposition offset, test vector); every rank receives it by
+    torch.distributed.broadcast — RCCL over xGMI for the nccl backend, one
+    bucket per tensor — and imports it.  Nothing else crosses devices: this
+    replaces the reference's per-process CloudKey.new (key.zig:70-77) on ranks
+    other than `src`.  Returns the number of bytes broadcast.
+
+    `ctx` needs key_blob_bytes / export_key_device / import_key_device /
+    params.N (tfhe_amd.Context; the gloo tests pass a host stand-in)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -34,13 +46,32 @@ def broadcast_cloud_key(ctx, device, src: int = 0, group=None):
     meta = torch.zeros(1 + 2 * ctx.params.N, dtype=torch.int64, device=device)
     if rank == src:
         offset, tv = ctx.export_key_device(bk.data_ptr(), ksk.data_ptr())
+        _sync(device)
         meta[0] = offset
-        meta[1:] = torch.from_numpy(tv.astype(np.int64))
+        meta[1:] = torch.from_numpy(np.asarray(tv).astype(np.int64))
     for t in (bk, ksk, meta):
         dist.broadcast(t, src, group=group)
     if rank != src:
-        torch.cuda.synchronize(device)
+        _sync(device)
         m = meta.cpu().numpy()
         ctx.import_key_device(bk.data_ptr(), ksk.data_ptr(), int(m[0]), m[1:].astype(np.uint32))
-    torch.cuda.synchronize(device)
+    _sync(device)
     return bk_bytes + ksk_bytes
+
+
+def sharded_gate_batch(ctx, ops, a, b, rank: int, world: int, gather: bool = True, group=None):
+    """Data-parallel gate batch: rank r bootstraps the contiguous slice
+    shard_range(B, r, world) of the global batch on its own GPU (no collective
+    on the data path).  With gather=True the slices are all-gathered (host
+    side, once, after the work) so every rank returns the whole batch's
+    outputs in order — what a single Gates.*Gate loop over the batch returns."""
+    import numpy as np
+
+    lo, hi = shard_range(len(ops), rank, world)
+    out = ctx.gate_batch(np.asarray(ops)[lo:hi], np.asarray(a)[lo:hi], np.asarray(b)[lo:hi])
+    if not gather or world == 1:
+        return out
+    import torch.distributed as dist
+    parts = [None] * world
+    dist.all_gather_object(parts, (lo, out), group=group)
+    return np.concatenate([o for _, o in sorted(parts, key=lambda x: x[0])], axis=0)
