@@ -1,0 +1,4 @@
+set -o pipefail
+for f in tools/bin/ko_*; do
+  echo "== $f"; timeout -k 10 60 $f 1024 | grep "rep 1" || exit 1
+done

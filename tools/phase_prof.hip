@@ -1,0 +1,62 @@
+// Development tool: per-phase s_memtime breakdown of the blind-rotation kernel
+// on a 1024-gate 128-bit batch with random operands (timing only, no parity).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DTFHE_PHASE_PROF \
+//         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
+#include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace tfhe;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+int main(int argc, char **argv) {
+    const size_t B = argc > 1 ? atoi(argv[1]) : 1024;
+    KParams P{700, 1024, 3, 6, 2, 9, 0x82080000u};
+    std::vector<double> bk((size_t)P.n * 2 * P.L * 2 * 1024);
+    srand(1);
+    for (auto &x : bk) x = (rand() / (double)RAND_MAX - 0.5) * 1e6;
+    std::vector<uint32_t> in((size_t)B * (P.n + 1)), tv(2048, 0x20000000u);
+    for (auto &x : in) x = (uint32_t)rand() * 2654435761u;
+    std::vector<C2> tw(512), twist(512);
+    for (int k = 0; k < 512; k++) {
+        twist[k] = {cos(k * (M_PI / 1024)), sin(k * (M_PI / 1024))};
+        tw[k] = {cos(k * 0.01), -sin(k * 0.01)};
+    }
+    double *d_bk; uint32_t *d_in, *d_tv, *d_out; C2 *d_tw, *d_twist;
+    CK(hipMalloc(&d_bk, bk.size() * 8));
+    CK(hipMalloc(&d_in, in.size() * 4));
+    CK(hipMalloc(&d_tv, 2048 * 4));
+    CK(hipMalloc(&d_out, B * 2048 * 4));
+    CK(hipMalloc(&d_tw, 512 * 16));
+    CK(hipMalloc(&d_twist, 512 * 16));
+    CK(hipMemcpy(d_bk, bk.data(), bk.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_in, in.data(), in.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_tv, tv.data(), 2048 * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_tw, tw.data(), 512 * 16, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_twist, twist.data(), 512 * 16, hipMemcpyHostToDevice));
+    DevTables T{d_twist, d_tw};
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int rep = 0; rep < 2; rep++) {
+        unsigned long long z[8] = {0};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
+        CK(hipEventRecord(e0));
+        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0));
+        CK(hipEventRecord(e1));
+        CK(hipDeviceSynchronize());
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+        unsigned long long c[8];
+        CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
+        const char *nm[8] = {"tmp", "fwd-fft(pairs)", "barrier1", "mac", "barrier2", "inverse+add", "tail", "dma-issue"};
+        double tot = 0;
+        for (int k = 0; k < 8; k++) tot += c[k];
+        printf("rep %d: %.3f ms; cycles per wave-step (s_memtime ticks):\n", rep, ms);
+        for (int k = 0; k < 8; k++)
+            printf("  %-16s %10.1f  %5.1f%%\n", nm[k], c[k] / (double)B / P.n, 100.0 * c[k] / tot);
+        printf("  total            %10.1f\n", tot / B / P.n);
+    }
+    return 0;
+}

@@ -29,6 +29,34 @@ namespace tfhe {
 
 #define DEV __device__ __forceinline__
 
+// Development-only phase timing of the blind-rotation kernels (tools/phase_prof.hip
+// defines TFHE_PHASE_PROF): s_memtime deltas per phase, summed per wave and
+// added to g_phase_cycles at the end.  Compiles to nothing otherwise.
+struct PhaseProf {
+#ifdef TFHE_PHASE_PROF
+    uint64_t last;
+    int cur;
+    uint64_t acc[8];
+    DEV void start() {
+        cur = 0;
+        for (int k = 0; k < 8; k++) acc[k] = 0;
+        last = __builtin_amdgcn_s_memtime();
+    }
+    DEV void mark(int k) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        acc[cur] += now - last;
+        last = now;
+        cur = k;
+    }
+#else
+    DEV void start() {}
+    DEV void mark(int) {}
+#endif
+};
+#ifdef TFHE_PHASE_PROF
+__device__ unsigned long long g_phase_cycles[8];
+#endif
+
 DEV C2 c2(double x, double y) {
     C2 r;
     r.x = x;
@@ -394,7 +422,9 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
         e[0][q] = fa[br3(q)];
         e[1][q] = fb[br3(q)];
     }
+#ifndef TFHE_KO_INV
     fft512_x2<true>(e, xb, T, t);
+#endif
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         double ra, ia, rb, ib;
@@ -491,7 +521,8 @@ DEV void load_digits_lds(C2 *d, const uint32_t *s_tmp, int row, int L, int bgbit
 // pair's BK rows in LDS, MAC, release the buffer and prefetch the next pair.
 template <int L>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
-                  C2 *fa, C2 *fb, double2 *s_bk, const double2 *__restrict__ next_pair, bool has_next) {
+                  C2 *fa, C2 *fb, double2 *s_bk, const double2 *__restrict__ next_pair, bool has_next,
+                  PhaseProf &pp) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
         fa[q] = c2(0.0, 0.0);
@@ -500,14 +531,31 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #pragma unroll 1
     for (int rp = 0; rp < L; rp++) {
         C2 d[2][8];
+        pp.mark(1);
         load_digits_lds(d[0], s_tmp, 2 * rp, L, bgbit, twist_t, t);
         load_digits_lds(d[1], s_tmp, 2 * rp + 1, L, bgbit, twist_t, t);
+#ifndef TFHE_KO_FFT  // TFHE_KO_*: development knock-out builds (timing only)
         fft512_x2<false>(d, xb, T, t);
+#endif
+        pp.mark(2);
+#ifndef TFHE_KO_BAR
         __syncthreads();  // BK pair has landed (s_waitcnt vmcnt(0) + s_barrier)
+#endif
+        pp.mark(3);
+#ifndef TFHE_KO_MAC
         mac_row<false>(fa, fb, d[0], s_bk, t);
         mac_row<false>(fa, fb, d[1], s_bk + 1024, t);
+#else
+        for (int q = 0; q < 8; q++) fa[q] = c2(fa[q].x + d[0][q].x, fa[q].y + d[1][q].y);
+#endif
+        pp.mark(4);
+#ifndef TFHE_KO_BAR
         __syncthreads();  // every wave is done reading the pair
+#endif
+        pp.mark(7);
+#ifndef TFHE_KO_DMA
         if (rp + 1 < L || has_next) issue_bk_pair(next_pair + (size_t)rp * 2048, s_bk, tid);
+#endif
     }
 }
 
@@ -566,8 +614,11 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     LdsTw T;
     T.init(s_tw);
     const C2 *twist_t = s_twist + t;  // twist of coefficient t + 64m at [64m]
+    PhaseProf pp;
+    pp.start();
 
     for (int i = 0; i < n; i++) {
+        pp.mark(0);
         // a~ in {0, 2N} gives tmp = 0 and an exactly-zero external product;
         // it is computed anyway so the four waves keep one barrier schedule.
         const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
@@ -576,8 +627,13 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         uint32_t tA[16], tB[16];
 #pragma unroll
         for (int m = 0; m < 16; m++) {
+#ifndef TFHE_KO_TMP
             tA[m] = rot_read(s_acc, t + 64 * m, at) - accA[m] + P.offset;
             tB[m] = rot_read(s_acc + 1024, t + 64 * m, at) - accB[m] + P.offset;
+#else
+            tA[m] = accA[m] * at + P.offset;
+            tB[m] = accB[m] * at + P.offset;
+#endif
         }
         wave_sync();
 #pragma unroll
@@ -588,7 +644,8 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         wave_sync();
         C2 fa[8], fb[8];
         br_pairs<L>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, bkd + (size_t)i * step_stride + 2048,
-                    i + 1 < n);
+                    i + 1 < n, pp);
+        pp.mark(5);
         inverse_and_add<SMALL, 64>(fa, fb, s_x, T, twist_t, t, accA, accB);
         wave_sync();
 #pragma unroll
@@ -598,6 +655,11 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         }
         wave_sync();
     }
+    pp.mark(6);
+#ifdef TFHE_PHASE_PROF
+    if (t == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], (unsigned long long)pp.acc[k]);
+#endif
 
     if (!valid) return;
     if (out_mode == BR_OUT_LV1) {
