@@ -81,8 +81,11 @@ def test_external_product_vs_oracle(oracle, pname):
     assert np.array_equal(c.external_product(x, bk_index=5), want)
 
 
-@pytest.mark.parametrize("pname,B", [("128", 9), ("80", 1), ("uint4", 17)])
-def test_key_switch_vs_oracle(oracle, pname, B):
+@pytest.mark.parametrize("form", ["lanes", "sel"])
+@pytest.mark.parametrize("pname,B", [("128", 9), ("128", 130), ("80", 1), ("80", 65), ("uint4", 17)])
+def test_key_switch_vs_oracle(oracle, pname, B, form, monkeypatch):
+    """Both key-switch forms (lane = item / lane = word) bit-exact, ragged B."""
+    monkeypatch.setenv("TFHE_KS_KERNEL", form)
     c, k = ctx_for(oracle, pname)
     lv1 = u32rand(rng(5), B, 1025)
     want = np.array([oracle.identity_key_switch(k.p, v, k.ck.ksk) for v in lv1])

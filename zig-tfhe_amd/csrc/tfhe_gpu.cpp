@@ -36,7 +36,7 @@ struct tfhe_gpu_ctx {
     std::vector<uint32_t> testvec;  // host copy, 2N
     uint32_t *d_testvec = nullptr;  // cloud testvec (2N)
     double *d_bk = nullptr;         // device layout, n*2L*512 double4
-    uint32_t *d_ksk = nullptr;      // reference layout
+    uint32_t *d_ksk = nullptr;      // reference rows padded to K.ks_stride words (ksk_dev_bytes)
     size_t bk_bytes = 0, ksk_bytes = 0;
     // scratch, grown on demand
     DevBuf s_a, s_b, s_out, s_lv1, s_ops, s_tv, s_tmp;
@@ -96,7 +96,21 @@ DevTables tables(const tfhe_gpu_ctx *c) { return DevTables{c->d_twist, c->d_tw};
 
 size_t tlwe0_words(const tfhe_gpu_ctx *c) { return (size_t)c->P.n + 1; }
 size_t bk_rows(const tfhe_params &p) { return (size_t)p.n * 2 * p.L; }
-size_t ksk_words(const tfhe_params &p) { return (size_t)p.N * p.iks_t * (1u << p.basebit) * (p.n + 1); }
+size_t ksk_rows(const tfhe_params &p) { return (size_t)p.N * p.iks_t * (1u << p.basebit); }
+size_t ksk_words(const tfhe_params &p) { return ksk_rows(p) * (p.n + 1); }
+// device KSK: padded rows + zero tail (tfhe_internal.hpp)
+size_t ksk_dev_bytes(const tfhe_params &p) {
+    return (ksk_rows(p) * ks_stride_for((int)p.n) + KS_TAIL_WORDS) * sizeof(uint32_t);
+}
+
+// host KSK (reference layout) -> device KSK (padded rows), async on the ctx stream
+int upload_ksk(tfhe_gpu_ctx *c, const uint32_t *ksk) {
+    const size_t w = c->P.n + 1, stride = c->K.ks_stride;
+    HIPCHK(c, hipMemsetAsync(c->d_ksk, 0, c->ksk_bytes, c->stream));
+    HIPCHK(c, hipMemcpy2DAsync(c->d_ksk, stride * 4, ksk, w * 4, w * 4, ksk_rows(c->P), hipMemcpyHostToDevice,
+                               c->stream));
+    return TFHE_OK;
+}
 
 int set_key_common(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv_a, const uint32_t *tv_b) {
     const uint32_t N = c->P.N;
@@ -109,7 +123,7 @@ int set_key_common(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv_a, const
                              c->stream));
     if (!c->d_bk) {
         c->bk_bytes = bk_rows(c->P) * 2048 * sizeof(double);
-        c->ksk_bytes = ksk_words(c->P) * sizeof(uint32_t);
+        c->ksk_bytes = ksk_dev_bytes(c->P);
         hipError_t e = hipMalloc((void **)&c->d_bk, c->bk_bytes);
         if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, "hipMalloc(bk)");
         e = hipMalloc((void **)&c->d_ksk, c->ksk_bytes);
@@ -207,7 +221,7 @@ int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
     c->P = *params;
     c->device = device;
     c->K = KParams{(int)params->n, (int)params->N, (int)params->L, (int)params->bgbit, (int)params->basebit,
-                   (int)params->iks_t, 0};
+                   (int)params->iks_t, 0, ks_stride_for((int)params->n)};
     int rc = TFHE_OK;
     do {
         hipError_t e = hipSetDevice(device);
@@ -287,7 +301,8 @@ int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv
     rc = h2d(c, c->s_tmp, bsk, bsk_len * sizeof(double));
     if (rc) return rc;
     HIPCHK(c, launch_bk_permute(c->K, (const double *)c->s_tmp.p, c->d_bk, rows, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk, c->ksk_bytes, hipMemcpyHostToDevice, c->stream));
+    rc = upload_ksk(c, ksk);
+    if (rc) return rc;
     HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));  // reference leaves k=0 rows undefined
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
@@ -297,7 +312,7 @@ int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv
 int tfhe_gpu_key_blob_bytes(const tfhe_gpu_ctx *c, size_t *bsk_bytes, size_t *ksk_bytes) {
     if (!c || !bsk_bytes || !ksk_bytes) return TFHE_ERR_INVALID;
     *bsk_bytes = bk_rows(c->P) * 2048 * sizeof(double);
-    *ksk_bytes = ksk_words(c->P) * sizeof(uint32_t);
+    *ksk_bytes = ksk_dev_bytes(c->P);  // device layout (padded rows), not the reference's
     return TFHE_OK;
 }
 
@@ -409,11 +424,12 @@ int tfhe_gpu_keygen(tfhe_gpu_ctx *c, uint64_t secret_seed, uint64_t cloud_seed, 
     rc = set_key_common(c, offset, tv.data(), tv.data() + N);
     if (rc) return rc;
     HIPCHK(c, launch_bk_permute(c->K, (const double *)c->s_tmp.p, c->d_bk, R, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk.data(), c->ksk_bytes, hipMemcpyHostToDevice, c->stream));
+    rc = upload_ksk(c, ksk.data());
+    if (rc) return rc;
     if (bsk_out)
         HIPCHK(c, hipMemcpyAsync(bsk_out, c->s_tmp.p, R * 2 * N * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (ksk_out) std::memcpy(ksk_out, ksk.data(), c->ksk_bytes);
+    if (ksk_out) std::memcpy(ksk_out, ksk.data(), ksk.size() * sizeof(uint32_t));
     c->has_key = true;
     return TFHE_OK;
 }

@@ -22,7 +22,14 @@ struct KParams {
     int basebit;    // key-switch base bits
     int iks_t;      // key-switch levels
     uint32_t offset;  // decomposition offset (key.zig:121-131)
+    int ks_stride;    // words per device KSK row: n+1 rounded up to 4 (16-B aligned rows)
 };
+
+// Device KSK: the reference's rows [(2^basebit*t*i) + 2^basebit*j + k] of
+// n+1 words (key.zig:148-172), each padded to ks_stride words, plus a tail of
+// KS_TAIL_WORDS zero words so chunked 16-B loads of the last row stay inside.
+constexpr int KS_TAIL_WORDS = 64;
+inline int ks_stride_for(int n) { return (n + 1 + 3) & ~3; }
 
 // Output forms of the blind-rotation kernel.
 enum BrOut : int {
@@ -48,6 +55,7 @@ hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32
                              uint32_t *out, size_t B, hipStream_t s);
 // zero the k = 0 rows (never read by the reference; the kernels subtract them unconditionally)
 hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s);
+// key-switch kernel form: 0 = lanes (default), 1 = select/gather (development knob TFHE_KS_KERNEL)
 hipError_t launch_fft_forward(const DevTables &T, const uint32_t *in, double *out, size_t B,
                               hipStream_t s);
 hipError_t launch_fft_inverse(const DevTables &T, const double *in, uint32_t *out, size_t B,

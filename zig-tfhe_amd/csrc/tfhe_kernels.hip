@@ -884,7 +884,8 @@ __global__ __launch_bounds__(256) void k_key_switch_sel(KParams P, const uint32_
 #pragma unroll
     for (int g = 0; g < G; g++) res[g] = (w == P.n && g0 + g < B) ? lv1[(g0 + g) * 1025 + 1024] : 0u;
     const uint32_t prec = 1u << (32 - (1 + 2 * T));
-    const size_t stride_i = (size_t)T * 4 * n1;
+    const size_t rs = (size_t)P.ks_stride;
+    const size_t stride_i = (size_t)T * 4 * rs;
     const uint32_t *rows0 = ksk + wc;
     for (int i0 = 0; i0 < 1024; i0 += 64) {
         // packed digits of a_{i0+lane} for every item: pkv[g] in lane l is item g's i0+l
@@ -900,7 +901,7 @@ __global__ __launch_bounds__(256) void k_key_switch_sel(KParams P, const uint32_
 #pragma unroll
             for (int j = 0; j < T; j++)
 #pragma unroll
-                for (int k = 0; k < 3; k++) r[j][k] = rows[(size_t)(4 * j + k + 1) * n1];
+                for (int k = 0; k < 3; k++) r[j][k] = rows[(size_t)(4 * j + k + 1) * rs];
 #pragma unroll
             for (int g = 0; g < G; g++) {
                 const uint32_t pk = __builtin_amdgcn_readlane(pkv[g], ii);
@@ -938,7 +939,8 @@ __global__ __launch_bounds__(256) void k_key_switch_gather(KParams P, const uint
 #pragma unroll
     for (int g = 0; g < G; g++) res[g] = (w == P.n && g0 + g < B) ? lv1[(g0 + g) * 1025 + 1024] : 0u;
     const uint32_t prec = 1u << (32 - (1 + basebit * T));
-    const size_t stride_i = (size_t)T * base * n1;
+    const size_t rs = (size_t)P.ks_stride;
+    const size_t stride_i = (size_t)T * base * rs;
     const uint32_t *rows0 = ksk + wc;
     for (int i0 = 0; i0 < 1024; i0 += 64) {
         uint32_t pkv[G];
@@ -957,7 +959,7 @@ __global__ __launch_bounds__(256) void k_key_switch_gather(KParams P, const uint
 #pragma unroll
                 for (int j = 0; j < T; j++) {
                     const uint32_t k = (pk >> (basebit * (T - 1 - j))) & (uint32_t)(base - 1);
-                    v[g][j] = rows[(size_t)(base * j + k) * n1];
+                    v[g][j] = rows[(size_t)(base * j + k) * rs];
                 }
             }
 #pragma unroll
@@ -973,12 +975,129 @@ __global__ __launch_bounds__(256) void k_key_switch_gather(KParams P, const uint
     }
 }
 
-// Zero the k = 0 rows of a KSK (left undefined by the reference, key.zig:156).
-__global__ void k_ksk_zero_k0(uint32_t *__restrict__ ksk, int n1, int base, size_t groups) {
+// Zero the k = 0 rows of a device KSK (left undefined by the reference, key.zig:156).
+__global__ void k_ksk_zero_k0(uint32_t *__restrict__ ksk, int rs, int base, size_t groups) {
     size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= groups * n1) return;
-    size_t grp = idx / n1, x = idx % n1;
-    ksk[grp * base * n1 + x] = 0u;
+    if (idx >= groups * rs) return;
+    size_t grp = idx / rs, x = idx % rs;
+    ksk[grp * base * rs + x] = 0u;
+}
+
+// Lane form (any base; default): lane = item (64 items per block), block =
+// one chunk of KL_CHUNK output words x all N*t digits, the 4 waves splitting
+// the coefficient range i and reducing through LDS at the end.  Per i, a wave
+// LDS-DMAs the chunk of all 2^basebit candidate rows of all t levels
+// ([j][16-B piece][k] slots; the zero k = 0 rows come along) into a private
+// double buffer, and every lane subtracts its digit's slots.  One KSK row
+// chunk serves 64 items (the select form's 8), and the candidates of one (j,
+// piece) sit in consecutive 16-B slots, so the lane-dependent ds_read_b128
+// touch distinct banks.
+constexpr int KL_CHUNK = 32;  // output words per block (8 pieces of 16 B)
+constexpr int KL_WAVES = 4;
+
+template <int T, int BASEBIT>
+__global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint32_t *__restrict__ lv1,
+                                                          const uint32_t *__restrict__ ksk,
+                                                          uint32_t *__restrict__ out, size_t B) {
+    constexpr int BASE = 1 << BASEBIT;
+    constexpr int PIECES = KL_CHUNK / 4;
+    constexpr int SLOTS = T * PIECES * BASE;    // 16-B slots per coefficient i
+    constexpr int NDMA = (SLOTS + 63) / 64;     // LDS-DMA instructions per i
+    constexpr int BUF = NDMA * 64 + 16;         // 16-B slots per buffer: KSK slots + 64 digits words
+    constexpr int RING = 2 * BUF;               // double buffer
+    constexpr int RED = KL_WAVES * KL_CHUNK * 64;  // reduction words
+    constexpr int LDS_BYTES = (RING * 16 * KL_WAVES > RED * 4) ? RING * 16 * KL_WAVES : RED * 4;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4 *ring = reinterpret_cast<uint4 *>(smem) + w * RING;
+    const size_t g_raw = (size_t)blockIdx.y * 64 + lane;
+    const bool valid = g_raw < B;
+    const size_t g = valid ? g_raw : B - 1;
+    const int w0 = blockIdx.x * KL_CHUNK;
+    const size_t rs = (size_t)P.ks_stride;
+    const size_t step_i = (size_t)BASE * T * rs;  // words between consecutive i
+    const int ilo = w * (1024 / KL_WAVES), ihi = ilo + 1024 / KL_WAVES;
+    // this lane's DMA sources relative to row (i, 0, 0): slot s = c*64 + lane
+    uint32_t src_off[NDMA];
+#pragma unroll
+    for (int c = 0; c < NDMA; c++) {
+        const int sl = min(c * 64 + lane, SLOTS - 1);  // padding slots re-load the last one
+        const int k = sl % BASE, piece = (sl / BASE) % PIECES, j = sl / (BASE * PIECES);
+        src_off[c] = (uint32_t)((BASE * j + k) * rs + w0 + 4 * piece);
+    }
+    // Per i, one buffer receives the KSK slots and, by a 4-byte LDS-DMA, a_i
+    // of the 64 items (lane g's word).  The DMAs are inline asm
+    // (cdna_hip_programming.md §5.7): as builtins hipcc would guard every
+    // ds_read of one buffer with vmcnt(0) against the fill of the other, so
+    // their completion is counted by hand (vmcnt(0) at the top of step i, when
+    // only buffer i's fill is in flight).
+    const uint32_t ring_lds = (uint32_t)(size_t)(lds_void_t *)ring;
+    const uint32_t *a_src = lv1 + g * 1025;
+    auto issue = [&](int i, int which) {
+        const uint32_t *r = ksk + (size_t)i * step_i;
+#pragma unroll
+        for (int c = 0; c < NDMA; c++) {
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (which * BUF + c * 64) * 16);
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(r + src_off[c]), "s"(dst)
+                : "memory");
+        }
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (which * BUF + NDMA * 64) * 16);
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(a_src + i), "s"(dst)
+            : "memory");
+    };
+    const uint32_t prec = 1u << (32 - (1 + BASEBIT * T));
+    uint32_t acc[KL_CHUNK];
+#pragma unroll
+    for (int x = 0; x < KL_CHUNK; x++) acc[x] = 0u;
+    issue(ilo, 0);
+    for (int i = ilo; i < ihi; i++) {
+        const int cur = (i - ilo) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // buffer i landed
+        wave_sync();
+        if (i + 1 < ihi) issue(i + 1, cur ^ 1);
+        const uint4 *buf = ring + cur * BUF;
+        const uint32_t a = reinterpret_cast<const uint32_t *>(buf + NDMA * 64)[lane];
+        const uint32_t pk = (a + prec) >> (32 - BASEBIT * T);  // digit j at bits BASEBIT*(T-1-j)
+#pragma unroll
+        for (int j = 0; j < T; j++) {
+            const uint32_t k = (pk >> (BASEBIT * (T - 1 - j))) & (uint32_t)(BASE - 1);
+            const uint4 *sl = buf + j * PIECES * BASE + k;
+#pragma unroll
+            for (int pc = 0; pc < PIECES; pc++) {
+                const uint4 v = sl[pc * BASE];
+                acc[4 * pc + 0] -= v.x;
+                acc[4 * pc + 1] -= v.y;
+                acc[4 * pc + 2] -= v.z;
+                acc[4 * pc + 3] -= v.w;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this buffer's reads done before its re-fill
+    }
+    __syncthreads();  // every wave done with its ring: reuse LDS for the reduction
+    uint32_t *red = reinterpret_cast<uint32_t *>(smem);
+#pragma unroll
+    for (int x = 0; x < KL_CHUNK; x++) red[(w * KL_CHUNK + x) * 64 + lane] = acc[x];
+    __syncthreads();
+    const int n1 = P.n + 1;
+    constexpr int PER = KL_CHUNK / KL_WAVES;
+#pragma unroll
+    for (int y = 0; y < PER; y++) {
+        const int x = w * PER + y;
+        uint32_t r = 0u;
+#pragma unroll
+        for (int v = 0; v < KL_WAVES; v++) r += red[(v * KL_CHUNK + x) * 64 + lane];
+        const int word = w0 + x;
+        if (valid && word < n1) out[g * n1 + word] = (word == P.n ? a_src[1024] : 0u) + r;  // r = -(sum of rows)
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1183,6 +1302,24 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk, uint32_t *out,
                              size_t B, hipStream_t s) {
     if (B == 0) return hipSuccess;
+    // kernel form: lanes (default) or the select/gather forms (TFHE_KS_KERNEL=sel, A/B and tests)
+    const char *form = getenv("TFHE_KS_KERNEL");
+    if (!(form && form[0] == 's')) {
+        dim3 grid((unsigned)((P.ks_stride + KL_CHUNK - 1) / KL_CHUNK), (unsigned)((B + 63) / 64)), block(64 * KL_WAVES);
+#define KS_LANES(T_, BB_) hipLaunchKernelGGL((k_key_switch_lanes<T_, BB_>), grid, block, 0, s, P, lv1, ksk, out, B)
+        bool launched = true;
+        if (P.basebit == 2 && P.iks_t == 9) KS_LANES(9, 2);
+        else if (P.basebit == 2 && P.iks_t == 8) KS_LANES(8, 2);
+        else if (P.basebit == 2 && P.iks_t == 7) KS_LANES(7, 2);
+        else if (P.basebit == 3 && P.iks_t == 4) KS_LANES(4, 3);
+        else if (P.basebit == 4 && P.iks_t == 3) KS_LANES(3, 4);
+        else if (P.basebit == 4 && P.iks_t == 4) KS_LANES(4, 4);
+        else if (P.basebit == 5 && P.iks_t == 3) KS_LANES(3, 5);
+        else if (P.basebit == 5 && P.iks_t == 2) KS_LANES(2, 5);
+        else launched = false;  // other shapes: the general forms below
+#undef KS_LANES
+        if (launched) return hipGetLastError();
+    }
     // items per block: development knob TFHE_KS_G in {8, 16, 32} (default 8)
     static const int G = [] {
         const char *e = getenv("TFHE_KS_G");
@@ -1220,10 +1357,10 @@ hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32
 }
 
 hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s) {
-    const int n1 = P.n + 1, base = 1 << P.basebit;
+    const int rs = P.ks_stride, base = 1 << P.basebit;
     const size_t groups = (size_t)1024 * P.iks_t;
-    const size_t total = groups * n1;
-    hipLaunchKernelGGL(k_ksk_zero_k0, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ksk, n1, base,
+    const size_t total = groups * rs;
+    hipLaunchKernelGGL(k_ksk_zero_k0, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ksk, rs, base,
                        groups);
     return hipGetLastError();
 }
