@@ -44,6 +44,7 @@ enum {
     TFHE_GATE_NAND = 0, TFHE_GATE_OR = 1, TFHE_GATE_AND = 2, TFHE_GATE_XOR = 3,
     TFHE_GATE_XNOR = 4, TFHE_GATE_NOR = 5, TFHE_GATE_ANDNY = 6, TFHE_GATE_ANDYN = 7,
     TFHE_GATE_ORNY = 8, TFHE_GATE_ORYN = 9,
+    TFHE_GATE_NOT = 254,       /* circuits only: negation, no bootstrap (gates.zig:132-135) */
     TFHE_GATE_COPY = 255       /* no pre-combination: bootstrap input a as is */
 };
 
@@ -118,6 +119,18 @@ int tfhe_gpu_blind_rotate_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, const uin
  * identityKeySwitching with a LUT test vector (lut/generator.zig:85-135). */
 int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, const uint32_t *testvec,
                                  uint32_t *out, size_t B);
+
+/* ---- Circuits: level-scheduled gate DAG ----------------
+ * Replaces gate-by-gate evaluation of a circuit (examples/add_two_numbers.zig:
+ * 24-73, Gates.muxNaive gates.zig:124-129).  Wires 0..n_inputs-1 are the
+ * inputs (TLWELv0 each); gate g drives wire n_inputs+g from wires in_a[g],
+ * in_b[g] (both < n_inputs+g; in_b ignored for NOT/COPY).  ops: TFHE_GATE_*
+ * (bootstrapped) or TFHE_GATE_NOT (free).  Each dependency level is one
+ * batched bootstrap launch; every wire stays in HBM.  outputs receives the
+ * n_outputs wires out_wires[]; *levels (may be NULL) the bootstrap depth. */
+int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
+                          const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
+                          const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels);
 
 /* ---- Same, on device-resident buffers (async on the context stream) ---- */
 int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *ctx, const uint8_t *ops_dev, const uint32_t *a_dev,

@@ -1,0 +1,111 @@
+"""Level-scheduled circuits: tfhe_gpu_circuit_eval vs a
+gate-by-gate oracle evaluation, as the reference evaluates circuits
+(examples/add_two_numbers.zig:24-73, gates.zig:124-129 muxNaive)."""
+import numpy as np
+import pytest
+
+import tfhe_amd
+from tfhe_amd import Circuit
+
+
+def oracle_eval(oracle, keys, circ, inputs):
+    """Reference semantics: each gate is one Gates.*Gate call (bootstrap) or a
+    negation, evaluated in wire order."""
+    p = keys.p
+    wires = [np.asarray(x, np.uint32) for x in inputs]
+    for op, a, b in zip(circ.ops, circ.ia, circ.ib):
+        if op == tfhe_amd.NOT:
+            wires.append((0 - wires[a].astype(np.int64)).astype(np.uint32))
+        else:
+            wires.append(oracle.gate_batch(p, np.array([op], np.uint8), wires[a][None], wires[b][None], keys.ck)[0])
+    return np.array([wires[w] for w in circ.outputs])
+
+
+def test_circuit_builder_wires():
+    c = Circuit()
+    a, b, cin = c.input(), c.input(), c.input()
+    s, carry = c.full_adder(a, b, cin)
+    c.output(s, carry)
+    assert (a, b, cin) == (0, 1, 2)
+    assert c.ops == [tfhe_amd.XOR, tfhe_amd.AND, tfhe_amd.AND, tfhe_amd.XOR, tfhe_amd.OR]
+    assert c.outputs == [6, 7]
+    m = c.mux(a, b, cin)
+    assert c.ops[-4:] == [tfhe_amd.AND, tfhe_amd.NOT, tfhe_amd.AND, tfhe_amd.OR] and m == c.n_inputs + len(c.ops) - 1
+    with pytest.raises(ValueError):
+        c.input()  # inputs come first
+    with pytest.raises(ValueError):
+        c.and_(0, 999)
+
+
+@pytest.mark.gpu
+def test_circuit_adder_16bit_bit_exact(oracle):
+    """402 + 304 = 706 through one circuit launch sequence; every output word
+    equals the reference's gate-by-gate evaluation (80-bit keys)."""
+    from conftest import get_keys
+    k = get_keys(oracle, "80")
+    ctx = tfhe_amd.Context("80", 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    sk = tfhe_amd.SecretKey(ctx.params, k.k0, k.k1)
+    c = Circuit()
+    A = [c.input() for _ in range(16)]
+    Bw = [c.input() for _ in range(16)]
+    cin = c.input()
+    s, carry = c.ripple_add(A, Bw, cin)
+    c.output(*s, carry)
+    bits = [(402 >> i) & 1 for i in range(16)] + [(304 >> i) & 1 for i in range(16)] + [0]
+    inputs = sk.encrypt_bool(bits, seed0=77)
+    got, depth = c.run(ctx, inputs)
+    assert depth == 33  # carry chain: XOR then 2 levels per bit (AND, OR)
+    val = sum(int(x) << i for i, x in enumerate(sk.decrypt_bool(got[:16])))
+    assert val == 706 and not sk.decrypt_bool(got[16:])[0]
+    assert np.array_equal(got, oracle_eval(oracle, k, c, inputs))
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_circuit_mixed_gates_with_mux(oracle):
+    """Config-4-shaped workload: independent AND/OR/XOR/MUX gates (MUX = 3
+    bootstraps in 2 levels) over shared inputs, outputs bit-exact."""
+    from conftest import get_keys
+    k = get_keys(oracle, "80")
+    ctx = tfhe_amd.Context("80", 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    sk = tfhe_amd.SecretKey(ctx.params, k.k0, k.k1)
+    g = np.random.default_rng(5)
+    c = Circuit()
+    ins = [c.input() for _ in range(12)]
+    want_bits = []
+    bits = g.integers(0, 2, 12)
+    for _ in range(24):
+        kind = int(g.integers(0, 4))
+        x, y, z = (int(v) for v in g.choice(12, 3, replace=False))
+        if kind == 0: w = c.and_(ins[x], ins[y]); want_bits.append(bits[x] & bits[y])
+        elif kind == 1: w = c.or_(ins[x], ins[y]); want_bits.append(bits[x] | bits[y])
+        elif kind == 2: w = c.xor(ins[x], ins[y]); want_bits.append(bits[x] ^ bits[y])
+        else: w = c.mux(ins[x], ins[y], ins[z]); want_bits.append(bits[y] if bits[x] else bits[z])
+        c.output(w)
+    inputs = sk.encrypt_bool(bits.astype(np.uint8), seed0=500)
+    got, depth = c.run(ctx, inputs)
+    assert depth == 2
+    assert np.array_equal(sk.decrypt_bool(got), np.array(want_bits, bool))
+    assert np.array_equal(got, oracle_eval(oracle, k, c, inputs))
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_circuit_rejects_bad_graphs(oracle):
+    from conftest import get_keys
+    k = get_keys(oracle, "80")
+    ctx = tfhe_amd.Context("80", 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    x = np.zeros((2, ctx.params.n + 1), np.uint32)
+    with pytest.raises(RuntimeError):  # forward reference
+        ctx.circuit_eval(x, np.array([tfhe_amd.AND], np.uint8), np.array([0], np.uint32), np.array([2], np.uint32),
+                         np.array([2], np.uint32))
+    with pytest.raises(RuntimeError):  # unknown op
+        ctx.circuit_eval(x, np.array([77], np.uint8), np.array([0], np.uint32), np.array([1], np.uint32),
+                         np.array([2], np.uint32))
+    out, depth = ctx.circuit_eval(x, np.zeros(0, np.uint8), np.zeros(0, np.uint32), np.zeros(0, np.uint32),
+                                  np.array([1, 0], np.uint32))  # no gates: outputs are inputs
+    assert depth == 0 and np.array_equal(out, x[[1, 0]])
+    ctx.close()

@@ -1,0 +1,60 @@
+// Development micro-benchmark: throughput of the device FFT building blocks
+// (fft512_x2 / fft512<1>) at one wave per SIMD, registers only in/out.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Izig-tfhe_amd/csrc -o tools/bin/fft_bench tools/fft_bench.hip
+#include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
+#include <cstdio>
+using namespace tfhe;
+
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void k_bench(DevTables TT, double *out, int iters) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[8192 + 8192 + 4 * 16384];
+    C2 *s_tw = reinterpret_cast<C2 *>(smem);
+    C2 *s_twist = reinterpret_cast<C2 *>(smem + 8192);
+    const int tid = threadIdx.x, t = tid & 63, w = tid >> 6;
+    C2 *xb = reinterpret_cast<C2 *>(smem + 16384 + w * 16384);
+    for (int x = tid; x < 511; x += 256) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 256) s_twist[x] = TT.twist[x];
+    __syncthreads();
+    LdsTw T;
+    T.init(s_tw);
+    C2 d[2][8];
+    for (int q = 0; q < 8; q++) {
+        d[0][q] = c2(t * 0.001 + q, q * 0.5);
+        d[1][q] = c2(t * 0.002 - q, q * 0.25);
+    }
+    for (int it = 0; it < iters; it++) {
+        if (MODE == 0) fft512_x2<false>(d, xb, T, t);
+        if (MODE == 1) { fft512<1, false>(d, xb, T, t); fft512<1, false>(d + 1, xb, T, t); }
+        if (MODE == 2) { C2 w[7]; T.pass_b(w, t); passA<false>(d[0], T.a); passA<false>(d[1], T.a); passBC<false>(d[0], w); passBC<false>(d[1], w); passBC<false>(d[0], w); passBC<false>(d[1], w); }
+        if (MODE == 3) { passA<false>(d[0], T.a); passA<false>(d[1], T.a); ex1_write(d[0], xb, t); ex1_write(d[1], xb + 512, t); wave_sync(); ex1_read(d[0], xb, t); ex1_read(d[1], xb + 512, t); wave_sync();}
+    }
+    double s = 0;
+    for (int q = 0; q < 8; q++) s += d[0][q].x + d[1][q].y;
+    out[blockIdx.x * 256 + tid] = s;
+}
+
+int main() {
+    C2 *tw, *twist; double *out;
+    hipMalloc(&tw, 512 * 16); hipMalloc(&twist, 512 * 16); hipMalloc(&out, 2048 * 256 * 8);
+    std::vector<C2> h(512);
+    for (int k = 0; k < 512; k++) h[k] = {cos(k * 0.01), -sin(k * 0.01)};
+    hipMemcpy(tw, h.data(), 512 * 16, hipMemcpyHostToDevice);
+    hipMemcpy(twist, h.data(), 512 * 16, hipMemcpyHostToDevice);
+    DevTables T{twist, tw};
+    const int iters = 2000, blocks = 256;
+    hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+    const char *nm[4] = {"fft512_x2 (pair, pipelined)", "2 x fft512<1>", "passes only, no exchange", "passA + exchange only"};
+    for (int rep = 0; rep < 2; rep++)
+    for (int m = 0; m < 4; m++) {
+        hipEventRecord(a);
+        if (m == 0) hipLaunchKernelGGL(k_bench<0>, dim3(blocks), dim3(256), 0, 0, T, out, iters);
+        if (m == 1) hipLaunchKernelGGL(k_bench<1>, dim3(blocks), dim3(256), 0, 0, T, out, iters);
+        if (m == 2) hipLaunchKernelGGL(k_bench<2>, dim3(blocks), dim3(256), 0, 0, T, out, iters);
+        if (m == 3) hipLaunchKernelGGL(k_bench<3>, dim3(blocks), dim3(256), 0, 0, T, out, iters);
+        hipEventRecord(b); hipEventSynchronize(b);
+        float ms; hipEventElapsedTime(&ms, a, b);
+        // cycles per FFT per wave at 2.4 GHz (each iteration = 2 FFTs per wave)
+        if (rep) printf("%-32s %8.3f ms  %7.0f cycles per FFT per wave\n", nm[m], ms, ms * 1e-3 * 2.4e9 / (iters * 2.0));
+    }
+    return 0;
+}

@@ -44,7 +44,7 @@ int main(int argc, char **argv) {
         unsigned long long z[8] = {0};
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
         CK(hipEventRecord(e0));
-        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0));
+        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0));
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));

@@ -40,6 +40,7 @@ struct tfhe_gpu_ctx {
     size_t bk_bytes = 0, ksk_bytes = 0;
     // scratch, grown on demand
     DevBuf s_a, s_b, s_out, s_lv1, s_ops, s_tv, s_tmp;
+    DevBuf s_wires, s_cidx, s_cops;  // circuit evaluator: wire table, gather indices, op codes
     // device timing (tfhe_gpu_profile_begin/end): 3 events per bootstrap launch
     bool profiling = false;
     std::vector<hipEvent_t> events;
@@ -141,7 +142,8 @@ enum RunKind : int {
 
 // Blind rotation (+ key switch for RUN_BOOTSTRAP) over device buffers, async.
 int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b,
-                      const uint32_t *testvec_dev, uint32_t *out, size_t B, int kind) {
+                      const uint32_t *testvec_dev, uint32_t *out, size_t B, int kind,
+                      const uint32_t *idx = nullptr) {
     const bool key_switch = kind == RUN_BOOTSTRAP;
     const int out_mode = kind == RUN_BOOTSTRAP ? BR_OUT_LV1 : kind == RUN_TRLWE ? BR_OUT_TRLWE : BR_OUT_LV0_EXTRACT2;
     if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
@@ -160,7 +162,7 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
         c->ev_used += 3;
         HIPCHK(c, hipEventRecord(ev[0], c->stream));
     }
-    HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
+    HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, idx, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
                                   lv1, out_mode, B, c->stream));
     if (ev[1]) HIPCHK(c, hipEventRecord(ev[1], c->stream));
     if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream));
@@ -268,7 +270,8 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
-                    c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p})
+                    c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p,
+                    c->s_wires.p, c->s_cidx.p, c->s_cops.p})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -509,6 +512,107 @@ int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint
                                (uint32_t *)c->s_out.p, B, RUN_BOOTSTRAP);
     if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
     return rc;
+}
+
+// ---- Circuit evaluation with a level scheduler -------------
+// Wire w < n_inputs is input w; gate g drives wire n_inputs + g.  A
+// bootstrapped gate is ready one level after the later of its inputs; a NOT
+// (negation) is ready with its input.  The device wire table is laid out in
+// evaluation order — inputs | NOTs of level 0 | gates of level 1 | NOTs of
+// level 1 | ... — so each level's batch writes one contiguous run of slots,
+// and its inputs are gathered by index inside the blind-rotation prologue.
+int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
+                          const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
+                          const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels_out) {
+    if (!c || (n_inputs && !inputs) || (n_gates && (!ops || !in_a || !in_b)) || (n_outputs && (!out_wires || !outputs)))
+        return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    const size_t W = n_inputs + n_gates, w1 = tlwe0_words(c);
+    if (W > 0xFFFFFFFFull) return fail(c, TFHE_ERR_INVALID, "too many wires");
+    // levels
+    std::vector<uint32_t> ready(W, 0);
+    uint32_t max_level = 0;
+    for (size_t g = 0; g < n_gates; g++) {
+        const size_t w = n_inputs + g;
+        const int op = ops[g];
+        const bool bootstrapped = op <= TFHE_GATE_ORYN || op == TFHE_GATE_COPY;
+        if (!bootstrapped && op != TFHE_GATE_NOT) return fail(c, TFHE_ERR_INVALID, "unknown gate op");
+        if (in_a[g] >= w) return fail(c, TFHE_ERR_INVALID, "gate input a is not an earlier wire");
+        const bool two = op <= TFHE_GATE_ORYN;
+        if (two && in_b[g] >= w) return fail(c, TFHE_ERR_INVALID, "gate input b is not an earlier wire");
+        uint32_t r = ready[in_a[g]];
+        if (two) r = std::max(r, ready[in_b[g]]);
+        ready[w] = bootstrapped ? r + 1 : r;
+        max_level = std::max(max_level, ready[w]);
+    }
+    for (size_t o = 0; o < n_outputs; o++)
+        if (out_wires[o] >= W) return fail(c, TFHE_ERR_INVALID, "output wire out of range");
+    // groups in evaluation order: NOT(0), BS(1), NOT(1), ..., BS(max), NOT(max)
+    std::vector<std::vector<uint32_t>> bs(max_level + 1), nots(max_level + 1);
+    for (size_t g = 0; g < n_gates; g++) {
+        const uint32_t lv = ready[n_inputs + g];
+        (ops[g] == TFHE_GATE_NOT ? nots[lv] : bs[lv]).push_back((uint32_t)g);
+    }
+    std::vector<uint32_t> slot(W);
+    for (size_t w = 0; w < n_inputs; w++) slot[w] = (uint32_t)w;
+    uint32_t next = (uint32_t)n_inputs;
+    for (uint32_t lv = 0; lv <= max_level; lv++) {
+        for (uint32_t g : bs[lv]) slot[n_inputs + g] = next++;
+        for (uint32_t g : nots[lv]) slot[n_inputs + g] = next++;
+    }
+    // per-group gather indices and op codes, concatenated in evaluation order
+    std::vector<uint32_t> idx;
+    std::vector<uint8_t> cops;
+    idx.reserve(2 * n_gates + n_outputs);
+    for (uint32_t lv = 0; lv <= max_level; lv++) {
+        for (uint32_t g : bs[lv]) {
+            const bool two = ops[g] <= TFHE_GATE_ORYN;
+            idx.push_back(slot[in_a[g]]);
+            idx.push_back(two ? slot[in_b[g]] : slot[in_a[g]]);
+            cops.push_back(ops[g]);
+        }
+        for (uint32_t g : nots[lv]) idx.push_back(slot[in_a[g]]);
+    }
+    for (size_t o = 0; o < n_outputs; o++) idx.push_back(slot[out_wires[o]]);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->s_wires, std::max<size_t>(W, 1) * w1 * 4);
+    if (!rc) rc = ensure(c, c->s_cidx, std::max<size_t>(idx.size(), 1) * 4);
+    if (!rc) rc = ensure(c, c->s_cops, std::max<size_t>(cops.size(), 1));
+    if (!rc) rc = ensure(c, c->s_out, std::max<size_t>(n_outputs, 1) * w1 * 4);
+    if (rc) return rc;
+    uint32_t *wires = (uint32_t *)c->s_wires.p;
+    const uint32_t *d_idx = (const uint32_t *)c->s_cidx.p;
+    const uint8_t *d_ops = (const uint8_t *)c->s_cops.p;
+    if (n_inputs) HIPCHK(c, hipMemcpyAsync(wires, inputs, n_inputs * w1 * 4, hipMemcpyHostToDevice, c->stream));
+    if (!idx.empty())
+        HIPCHK(c, hipMemcpyAsync(c->s_cidx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, c->stream));
+    if (!cops.empty()) HIPCHK(c, hipMemcpyAsync(c->s_cops.p, cops.data(), cops.size(), hipMemcpyHostToDevice, c->stream));
+    size_t ip = 0, op_pos = 0, sp = n_inputs;
+    for (uint32_t lv = 0; lv <= max_level; lv++) {
+        const size_t nb = bs[lv].size(), nn = nots[lv].size();
+        if (nb) {
+            rc = run_bootstrap_dev(c, d_ops + op_pos, wires, wires, nullptr, wires + sp * w1, nb, RUN_BOOTSTRAP,
+                                   d_idx + ip);
+            if (rc) return rc;
+            ip += 2 * nb;
+            op_pos += nb;
+            sp += nb;
+        }
+        if (nn) {
+            HIPCHK(c, launch_tlwe_gather(c->K, wires, d_idx + ip, wires + sp * w1, nn, true, c->stream));
+            ip += nn;
+            sp += nn;
+        }
+    }
+    if (n_outputs) {
+        HIPCHK(c, launch_tlwe_gather(c->K, wires, d_idx + ip, (uint32_t *)c->s_out.p, n_outputs, false, c->stream));
+        rc = d2h_sync(c, outputs, c->s_out.p, n_outputs * w1 * 4);
+        if (rc) return rc;
+    } else {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (levels_out) *levels_out = max_level;
+    return TFHE_OK;
 }
 
 int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *c, const uint8_t *ops_dev, const uint32_t *a_dev, const uint32_t *b_dev,

@@ -47,10 +47,15 @@ struct DevTables {
 };
 
 // ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------
+// idx: NULL, or B pairs (a, b) of ciphertext indices into in_a / in_b (circuit gather)
 hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
-                               const uint32_t *in_a, const uint32_t *in_b,
+                               const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out,
                                int out_mode, size_t B, hipStream_t s);
+// dst[k] = (negate ? -1 : 1) * src[idx[k]] for k < count, n+1 words each
+// (TLWELv0.neg: gates.zig:132-135)
+hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint32_t *idx, uint32_t *dst,
+                              size_t count, bool negate, hipStream_t s);
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
                              uint32_t *out, size_t B, hipStream_t s);
 // zero the k = 0 rows (never read by the reference; the kernels subtract them unconditionally)

@@ -411,6 +411,38 @@ DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t) {
     }
 }
 
+// MAC of a row pair from LDS, software-pipelined one frequency group ahead:
+// the 4 BK words of group q+1 are read while group q's 32 flops issue, and a
+// scheduling fence per group keeps hipcc from hoisting all 32 reads (128
+// VGPRs) ahead of the arithmetic, which pushes the kernel into AGPR copies.
+DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 *bk, int t) {
+    double2 k[2][4];
+    k[0][0] = bk[t];
+    k[0][1] = bk[64 + t];
+    k[0][2] = bk[1024 + t];
+    k[0][3] = bk[1024 + 64 + t];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int c = q & 1;
+        if (q + 1 < 8) {
+            k[c ^ 1][0] = bk[(2 * q + 2) * 64 + t];
+            k[c ^ 1][1] = bk[(2 * q + 3) * 64 + t];
+            k[c ^ 1][2] = bk[1024 + (2 * q + 2) * 64 + t];
+            k[c ^ 1][3] = bk[1024 + (2 * q + 3) * 64 + t];
+        }
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const C2 x = r ? d1[q] : d0[q];
+            const double2 ka = k[c][2 * r], kb = k[c][2 * r + 1];
+            const C2 ta = c2(x.x * ka.x - x.y * ka.y, x.x * ka.y + x.y * ka.x);
+            const C2 tb = c2(x.x * kb.x - x.y * kb.y, x.x * kb.y + x.y * kb.x);
+            fa[q] = c2(fa[q].x + ta.x, fa[q].y + ta.y);
+            fb[q] = c2(fb[q].x + tb.x, fb[q].y + tb.y);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Inverse transforms of the two accumulated spectra (fft1024 x2) and the
 // CMUX add acc' = ExtProd + acc (trgsw.zig:277-281), lane-local.
 template <bool SMALL, int TS, class TW>
@@ -543,8 +575,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #endif
         pp.mark(3);
 #ifndef TFHE_KO_MAC
-        mac_row<false>(fa, fb, d[0], s_bk, t);
-        mac_row<false>(fa, fb, d[1], s_bk + 1024, t);
+        mac_pair_lds(fa, fb, d[0], d[1], s_bk, t);
 #else
         for (int q = 0; q < 8; q++) fa[q] = c2(fa[q].x + d[0][q].x, fa[q].y + d[1][q].y);
 #endif
@@ -562,7 +593,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 template <int L, bool SMALL>
 __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
-    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ testvec,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
     const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
     // one __shared__ array (a second one can make hipcc drain LDS-DMA early)
     __shared__ __attribute__((aligned(16))) unsigned char smem[BR_LDS_TOTAL];
@@ -581,8 +612,10 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     const size_t g_raw = (size_t)blockIdx.x * BR_WAVES + w;
     const bool valid = g_raw < B;
     const size_t g = valid ? g_raw : B - 1;  // ragged tail: compute a copy, store nothing
-    const uint32_t *A = in_a + g * (size_t)(n + 1);
-    const uint32_t *Bv = in_b ? in_b + g * (size_t)(n + 1) : A;
+    // idx (optional): item g reads ciphertexts idx[2g] of in_a and idx[2g+1] of in_b
+    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
+    const uint32_t *A = in_a + ia * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
     const int op = ops ? (int)ops[g] : 255;
     const size_t step_stride = (size_t)L * 2048;  // double2 per TRGSW (BK[i])
 
@@ -720,7 +753,7 @@ DEV C2 cmul_bk(C2 d, double2 k) { return c2(d.x * k.x - d.y * k.y, d.x * k.y + d
 template <int L, bool SMALL>
 __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
-    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ testvec,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
     const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[BS_LDS_TOTAL];
     const int tid = threadIdx.x;
@@ -742,8 +775,10 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
     const size_t g_raw = (size_t)blockIdx.x * BS_GATES + gs;
     const bool valid = g_raw < B;
     const size_t g = valid ? g_raw : B - 1;
-    const uint32_t *A = in_a + g * (size_t)(n + 1);
-    const uint32_t *Bv = in_b ? in_b + g * (size_t)(n + 1) : A;
+    // idx (optional): item g reads ciphertexts idx[2g] of in_a and idx[2g+1] of in_b
+    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
+    const uint32_t *A = in_a + ia * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
     const int op = ops ? (int)ops[g] : 255;
     const size_t trgsw = (size_t)2 * L * 1024;  // double2 per BK[i]
 
@@ -801,10 +836,15 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
                 d[0][q] = twist_in(digit_f64(src[64 * m], level, P.bgbit),
                                    digit_f64(src[64 * (m + 8)], level, P.bgbit), twist_t[64 * m]);
             }
+#ifndef TFHE_KO_FFT
             fft512<1, false>(d, s_x, T, t);
+#endif
 #pragma unroll
             for (int q = 0; q < 8; q++) s_x[t + 64 * q] = d[0][q];  // publish this row's spectrum
+#ifndef TFHE_KO_BAR
             __syncthreads();  // spectra of rows 2r, 2r+1 and BK rows 2r, 2r+1 are in LDS
+#endif
+#ifndef TFHE_KO_MAC
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const C2 t0 = cmul_bk(spec_0[t + 64 * q], s_bk[(2 * q + h) * 64 + t]);
@@ -812,7 +852,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
                 S[q] = c2(S[q].x + t0.x, S[q].y + t0.y);
                 S[q] = c2(S[q].x + t1.x, S[q].y + t1.y);
             }
+#else
+            for (int q = 0; q < 8; q++) S[q] = c2(S[q].x + d[0][q].x, S[q].y);
+#endif
+#ifndef TFHE_KO_BAR
             __syncthreads();  // spectra and BK rows consumed
+#endif
             if (r + 1 < L) issue_bk_rows(bkd + (size_t)i * trgsw + (size_t)(2 * r + 2) * 1024, s_bk, tid);
             else if (i + 1 < n) issue_bk_rows(bkd + (size_t)(i + 1) * trgsw, s_bk, tid);
         }
@@ -820,7 +865,9 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
         C2 e[1][8];
 #pragma unroll
         for (int q = 0; q < 8; q++) e[0][q] = S[br3(q)];
+#ifndef TFHE_KO_INV
         fft512<1, true>(e, s_x, T, t);
+#endif
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             double re, im;
@@ -1256,12 +1303,34 @@ __global__ void k_bk_permute(const double *__restrict__ ref, double2 *__restrict
     }
 }
 
+// Ciphertext gather dst[k] = (NEG ? -1 : 1) * src[idx[k]]: TLWELv0.neg
+// (tlwe.zig:120-239, gates.zig:132-135 notGate) is the circuit evaluator's
+// free NOT; the plain form collects its outputs.  One block per ciphertext.
+template <bool NEG>
+__global__ __launch_bounds__(256) void k_tlwe_gather(const uint32_t *__restrict__ src,
+                                                     const uint32_t *__restrict__ idx, uint32_t *__restrict__ dst,
+                                                     int n1) {
+    const uint32_t *x = src + (size_t)idx[blockIdx.x] * n1;
+    uint32_t *y = dst + (size_t)blockIdx.x * n1;
+    for (int j = threadIdx.x; j < n1; j += 256) y[j] = NEG ? 0u - x[j] : x[j];
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint32_t *idx, uint32_t *dst,
+                              size_t count, bool negate, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (negate)
+        hipLaunchKernelGGL(k_tlwe_gather<true>, dim3((unsigned)count), dim3(256), 0, s, src, idx, dst, P.n + 1);
+    else
+        hipLaunchKernelGGL(k_tlwe_gather<false>, dim3((unsigned)count), dim3(256), 0, s, src, idx, dst, P.n + 1);
+    return hipGetLastError();
+}
+
 hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
-                               const uint32_t *in_a, const uint32_t *in_b, const uint32_t *testvec,
-                               const double *bkd, uint32_t *out, int out_mode, size_t B,
+                               const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                               const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
                                hipStream_t s) {
     if (B == 0) return hipSuccess;
     const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
@@ -1283,11 +1352,11 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
 #define BR_LAUNCH(L_, S_)                                                                                         \
     do {                                                                                                          \
         if (split)                                                                                                \
-            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, testvec, \
-                               bk2, out, out_mode, B);                                                            \
+            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
+                               testvec, bk2, out, out_mode, B);                                                   \
         else                                                                                                      \
-            hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, testvec, bk2,  \
-                               out, out_mode, B);                                                                 \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,  \
+                               bk2, out, out_mode, B);                                                            \
     } while (0)
     switch (P.L) {
     case 1: if (small) BR_LAUNCH(1, true); else BR_LAUNCH(1, false); break;

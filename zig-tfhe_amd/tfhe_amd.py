@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libtfhe_gpu.so")
 
 # gate op codes, include/tfhe_gpu.h TFHE_GATE_* (gates.zig:48-121)
 NAND, OR, AND, XOR, XNOR, NOR, ANDNY, ANDYN, ORNY, ORYN = range(10)
+NOT = 254  # circuits only: negation, no bootstrap
 COPY = 255
 GATE_NAMES = {"nand": NAND, "or": OR, "and": AND, "xor": XOR, "xnor": XNOR, "nor": NOR,
               "andny": ANDNY, "andyn": ANDYN, "orny": ORNY, "oryn": ORYN}
@@ -79,6 +80,8 @@ _SIGS = {
     "tfhe_gpu_bootstrap_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_bootstrap_without_key_switch_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_gate_batch": (C.c_int, [vp, u8p, u32p, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_circuit_eval": (C.c_int, [vp, C.c_size_t, u32p, C.c_size_t, u8p, u32p, u32p, C.c_size_t, u32p, u32p,
+                                        C.POINTER(C.c_uint32)]),
     "tfhe_gpu_blind_rotate_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_bootstrap_lut_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_gate_batch_dev": (C.c_int, [vp, vp, vp, vp, vp, C.c_size_t]),
@@ -244,6 +247,20 @@ class Context:
                                                                         cts.shape[0]),
                    "bootstrap_without_key_switch_batch")
         return out
+
+    def circuit_eval(self, inputs, ops, in_a, in_b, out_wires):
+        """Level-scheduled gate DAG (tfhe_gpu_circuit_eval).  -> (outputs, bootstrap depth)."""
+        inputs, ip = _u32(np.asarray(inputs, np.uint32).reshape(-1, self.params.n + 1))
+        ops = np.ascontiguousarray(ops, np.uint8)
+        in_a, ap = _u32(in_a)
+        in_b, bp = _u32(in_b)
+        out_wires, op_ = _u32(out_wires)
+        out = np.zeros((out_wires.size, self.params.n + 1), np.uint32)
+        lv = C.c_uint32()
+        self.check(self.lib.tfhe_gpu_circuit_eval(self.h, inputs.shape[0], ip, ops.size, ops.ctypes.data_as(u8p), ap,
+                                                  bp, out_wires.size, op_, out.ctypes.data_as(u32p), C.byref(lv)),
+                   "circuit_eval")
+        return out, lv.value
 
     def gate_batch(self, ops, a, b):
         ops = np.ascontiguousarray(ops, dtype=np.uint8)
@@ -459,3 +476,77 @@ class Gates:
         mu = 0x20000000  # f64ToTorus(0.125)
         res[-1] = mu if value else (1 - mu) & 0xFFFFFFFF
         return res
+
+
+class Circuit:
+    """Gate DAG builder for Context.circuit_eval: the
+    reference's circuits are sequences of Gates calls (gates.zig:48-151,
+    examples/add_two_numbers.zig:24-73); here they are recorded as wires and
+    evaluated level by level, one batched bootstrap launch per level.
+
+        c = Circuit(); a, b = c.input(), c.input(); s = c.xor(a, b); c.output(s)
+        outs, depth = c.run(ctx, [ct_a, ct_b])
+    """
+
+    def __init__(self):
+        self.n_inputs = 0
+        self.ops, self.ia, self.ib = [], [], []
+        self.outputs = []
+
+    def input(self) -> int:
+        if self.ops:
+            raise ValueError("declare every input before the first gate")
+        self.n_inputs += 1
+        return self.n_inputs - 1
+
+    def gate(self, op: int, a: int, b: int | None = None) -> int:
+        w = self.n_inputs + len(self.ops)
+        if not (0 <= a < w) or (b is not None and not (0 <= b < w)):
+            raise ValueError("gate inputs must be existing wires")
+        self.ops.append(op)
+        self.ia.append(a)
+        self.ib.append(a if b is None else b)
+        return w
+
+    # gates.zig:48-151
+    def nand(self, a, b): return self.gate(NAND, a, b)
+    def or_(self, a, b): return self.gate(OR, a, b)
+    def and_(self, a, b): return self.gate(AND, a, b)
+    def xor(self, a, b): return self.gate(XOR, a, b)
+    def xnor(self, a, b): return self.gate(XNOR, a, b)
+    def nor(self, a, b): return self.gate(NOR, a, b)
+    def and_ny(self, a, b): return self.gate(ANDNY, a, b)
+    def and_yn(self, a, b): return self.gate(ANDYN, a, b)
+    def or_ny(self, a, b): return self.gate(ORNY, a, b)
+    def or_yn(self, a, b): return self.gate(ORYN, a, b)
+    def not_(self, a): return self.gate(NOT, a)
+    def copy(self, a): return self.gate(COPY, a)
+
+    def mux(self, a, b, c):
+        """muxNaive (gates.zig:124-129): OR(AND(a, b), AND(NOT a, c)) — 2 bootstrap levels."""
+        return self.or_(self.and_(a, b), self.and_(self.not_(a), c))
+
+    def full_adder(self, a, b, cin):
+        """examples/add_two_numbers.zig:24-47: (sum, carry)."""
+        x = self.xor(a, b)
+        ab = self.and_(a, b)
+        xc = self.and_(x, cin)
+        return self.xor(x, cin), self.or_(ab, xc)
+
+    def ripple_add(self, a_bits, b_bits, cin):
+        """examples/add_two_numbers.zig:50-73: LSB-first bit wires -> (sum wires, carry)."""
+        out, carry = [], cin
+        for a, b in zip(a_bits, b_bits):
+            s, carry = self.full_adder(a, b, carry)
+            out.append(s)
+        return out, carry
+
+    def output(self, *wires):
+        self.outputs.extend(wires)
+
+    def run(self, ctx: "Context", inputs):
+        inputs = np.asarray(inputs, np.uint32).reshape(-1, ctx.params.n + 1)
+        if inputs.shape[0] != self.n_inputs:
+            raise ValueError(f"circuit has {self.n_inputs} inputs, got {inputs.shape[0]}")
+        return ctx.circuit_eval(inputs, np.array(self.ops, np.uint8), np.array(self.ia, np.uint32),
+                                np.array(self.ib, np.uint32), np.array(self.outputs, np.uint32))
