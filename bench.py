@@ -8,6 +8,12 @@ generated on rank 0 and broadcast once over RCCL/xGMI; no collective on the
 data path.  Rank 0 prints one JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--params 128]
+
+Other BASELINE configs (parity cases; these print their own line, never the
+default one): --workload adder (config 3: 16-bit ripple-carry adder, one
+circuit = 80 gates in 33 levels, and --batch independent adders side by side),
+mixed (config 4: --batch gates per GPU, op uniform over AND/OR/XOR/MUX),
+lut (config 5: UINT4 programmable bootstrap, --batch 4096).
 """
 from __future__ import annotations
 
@@ -87,6 +93,110 @@ def cpu_baseline(p, sk, bk, ksk, A, B, gpu_out, seconds: float):
             "parity_spot_check": {"gates": nchk, "bit_exact": spot_ok}}
 
 
+def timed(fn, steps, warmup, world, device):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = fn()
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        st = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        el = float(st[0])
+    return el, out
+
+
+def run_workload(args, rank, world, device):
+    """Configs 3-5 of BASELINE.json (host-buffer APIs: PCIe copies included)."""
+    pname = "uint4" if args.workload == "lut" else args.params
+    ctx = tfhe_amd.Context(pname, device.index)
+    p = ctx.params
+    if rank == 0:
+        sk, _ = ctx.keygen(42, 43)
+    if world > 1:
+        tdist.broadcast_cloud_key(ctx, device)
+        kbuf = torch.zeros(p.n + p.N, dtype=torch.int64, device=device)
+        if rank == 0:
+            kbuf[:] = torch.from_numpy(np.concatenate([sk.key_lv0, sk.key_lv1]).astype(np.int64))
+        dist.broadcast(kbuf, 0)
+        kk = kbuf.cpu().numpy().astype(np.uint32)
+        sk = tfhe_amd.SecretKey(p, kk[:p.n], kk[p.n:])
+    g = np.random.default_rng(2000 + rank)
+    extra = {}
+    if args.workload == "adder":
+        nadd = args.batch
+        c = tfhe_amd.Circuit()
+        wa = [[c.input() for _ in range(16)] for _ in range(nadd)]
+        wb = [[c.input() for _ in range(16)] for _ in range(nadd)]
+        wc = [c.input() for _ in range(nadd)]
+        for k in range(nadd):
+            sm, carry = c.ripple_add(wa[k], wb[k], wc[k])
+            c.output(*sm)
+        xa, xb = g.integers(0, 1 << 16, nadd), g.integers(0, 1 << 16, nadd)
+        xa[0], xb[0] = 402, 304
+        bits = np.concatenate([((xa[:, None] >> np.arange(16)) & 1).ravel(), ((xb[:, None] >> np.arange(16)) & 1).ravel(),
+                               np.zeros(nadd, np.int64)]).astype(np.uint8)
+        inputs = sk.encrypt_bool(bits, seed0=1)
+        el, (outs, depth) = timed(lambda: c.run(ctx, inputs), args.steps, args.warmup, world, device)
+        dec = sk.decrypt_bool(outs).reshape(nadd, 16)
+        vals = (dec.astype(np.int64) << np.arange(16)).sum(1)
+        ok = bool(np.array_equal(vals, (xa + xb) & 0xFFFF)) and int(vals[0]) == 706
+        units = len(c.ops) * world * args.steps  # every adder gate is a bootstrap
+        metric, unit = "gate-bootstraps/sec (16-bit ripple-carry adders, level-scheduled circuit)", "gate-bootstraps/s"
+        extra = {"adders_per_step": nadd * world, "gates_per_adder": len(c.ops) // nadd, "levels": depth,
+                 "ms_per_adder_circuit": round(el / args.steps * 1e3, 3), "sums_check": ok}
+        workload = f"{nadd} independent 16-bit ripple-carry adders per GPU (examples/add_two_numbers.zig), 402+304 first"
+    elif args.workload == "mixed":
+        B = args.batch
+        c = tfhe_amd.Circuit()
+        ins = [c.input() for _ in range(3 * B)]
+        kinds = g.integers(0, 4, B)
+        bits = g.integers(0, 2, 3 * B).astype(np.uint8)
+        want = np.empty(B, bool)
+        for k in range(B):
+            x, y, z = ins[3 * k], ins[3 * k + 1], ins[3 * k + 2]
+            bx, by, bz = bits[3 * k], bits[3 * k + 1], bits[3 * k + 2]
+            if kinds[k] == 0: c.output(c.and_(x, y)); want[k] = bx & by
+            elif kinds[k] == 1: c.output(c.or_(x, y)); want[k] = bx | by
+            elif kinds[k] == 2: c.output(c.xor(x, y)); want[k] = bx ^ by
+            else: c.output(c.mux(x, y, z)); want[k] = by if bx else bz
+        inputs = sk.encrypt_bool(bits, seed0=1)
+        el, (outs, depth) = timed(lambda: c.run(ctx, inputs), args.steps, args.warmup, world, device)
+        ok = bool(np.array_equal(sk.decrypt_bool(outs), want))
+        n_boot = int(sum(1 for op in c.ops if op != tfhe_amd.NOT))
+        units = B * world * args.steps
+        metric, unit = "gates/sec (mixed AND/OR/XOR/MUX, 128-bit)", "gates/s"
+        extra = {"bootstraps_per_sec": round(n_boot * world * args.steps / el, 2), "levels": depth,
+                 "decrypt_check": ok}
+        workload = f"{B} gates per GPU, op uniform over AND/OR/XOR/MUX (MUX = 3 bootstraps, 2 levels)"
+    else:  # lut
+        B = args.batch
+        m = 16
+        tv = tfhe_amd.lut_generate(p, m, lambda x: (x * x + 3) % m)
+        msgs = g.integers(0, m, B).astype(np.uint32)
+        cts = sk.encrypt_lwe_message(msgs, m, seed0=1)
+        el, outs = timed(lambda: ctx.bootstrap_lut_batch(cts, tv), args.steps, args.warmup, world, device)
+        ok = bool(np.array_equal(sk.decrypt_lwe_message(outs, m), (msgs * msgs + 3) % m))
+        units = B * world * args.steps
+        metric, unit = "programmable bootstraps/sec (UINT4 LUT)", "bootstraps/s"
+        extra = {"decrypt_check": ok}
+        workload = f"{B} UINT4 LUT bootstraps per GPU (f(x) = x^2+3 mod 16; n=820, L=1, Bg=2^22, t=3, basebit 5)"
+    if rank == 0:
+        line = {"metric": metric, "value": round(units / el, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded keys and inputs)",
+                "config": {"workload": workload, "params": pname, "parallelism": f"dp{world}"}}
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,6 +206,8 @@ def main():
     ap.add_argument("--params", default="128")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="nand", choices=["nand", "adder", "mixed", "lut"],
+                    help="nand = the headline metric (default); others: BASELINE configs 3-5")
     args = ap.parse_args()
 
     rank, world, local = tdist.env_rank_world()
@@ -103,6 +215,11 @@ def main():
         dist.init_process_group("nccl")  # RCCL
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    if args.workload != "nand":
+        run_workload(args, rank, world, device)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     ctx = tfhe_amd.Context(args.params, local)
     p = ctx.params
