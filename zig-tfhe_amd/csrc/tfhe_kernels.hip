@@ -246,9 +246,12 @@ DEV void ex2_read(C2 *d, const C2 *xb, int t) {
 // LDS exchange (write burst, in-order read-back) overlaps the other one's
 // butterfly pass: the wave always has VALU work while its DS queue drains.
 // Same arithmetic as fft512<2, INV>.
-template <bool INV, class TW>
+// ONEBUF: both transforms exchange through one 8 KB buffer.  Every write
+// into it follows, in this wave's program order, the reads of the data it
+// overwrites, and one wave's LDS operations execute in order.
+template <bool INV, bool ONEBUF = false, class TW>
 DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
-    C2 *x0 = xb, *x1 = xb + 512;
+    C2 *x0 = xb, *x1 = ONEBUF ? xb : xb + 512;
     C2 wb_[7], wc_[7];
     passA<INV>(d[0], T.a);
     ex1_write(d[0], x0, t);
@@ -445,7 +448,7 @@ DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 
 
 // Inverse transforms of the two accumulated spectra (fft1024 x2) and the
 // CMUX add acc' = ExtProd + acc (trgsw.zig:277-281), lane-local.
-template <bool SMALL, int TS, class TW>
+template <bool SMALL, int TS, bool ONEBUF = false, class TW>
 DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const C2 *tws, int t,
                          uint32_t *accA, uint32_t *accB) {
     C2 e[2][8];
@@ -455,7 +458,7 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
         e[1][q] = fb[br3(q)];
     }
 #ifndef TFHE_KO_INV
-    fft512_x2<true>(e, xb, T, t);
+    fft512_x2<true, ONEBUF>(e, xb, T, t);
 #endif
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -525,11 +528,11 @@ DEV void issue_bk_pair(const double2 *__restrict__ src, double2 *lds, int tid) {
 // live in wave-private LDS and need no block barrier.
 // ---------------------------------------------------------------------------
 constexpr int BR_WAVES = 4;
-constexpr int BR_LDS_BK = 2048 * 16;                  // one row pair, double2
+constexpr int BR_LDS_BK = 2 * 2048 * 16;              // two row-pair slots, double2
 constexpr int BR_LDS_TW = 512 * 16;                   // stage twiddles (511 used)
 constexpr int BR_LDS_TWIST = 512 * 16;                // twist factors
 constexpr int BR_LDS_ACC = 2048 * 4;                  // per wave
-constexpr int BR_LDS_X = 2 * 512 * 16;                // per wave, NF = 2
+constexpr int BR_LDS_X = 512 * 16;                    // per wave, one exchange buffer for both FFTs
 constexpr int BR_LDS_AT = 1024 * 2;                   // per wave
 constexpr int BR_LDS_TOTAL =
     BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST + BR_WAVES * (BR_LDS_ACC + BR_LDS_X + BR_LDS_AT);
@@ -551,9 +554,27 @@ DEV void load_digits_lds(C2 *d, const uint32_t *s_tmp, int row, int L, int bgbit
 
 // Row pairs of one CMUX step: forward FFTs of rows (2rp, 2rp+1), wait for the
 // pair's BK rows in LDS, MAC, release the buffer and prefetch the next pair.
+// LDS-DMA of one BK row pair (32 KB) into a slot, 8 x 16 B per thread, in
+// inline asm (cdna_hip_programming.md §5.7) so that hipcc does not guard the
+// MAC's reads of the other slot with vmcnt(0); completion is waited for by
+// hand before the block barrier that publishes the slot.
+DEV void issue_bk_pair_async(const double2 *__restrict__ src, double2 *slot, int tid) {
+    const uint32_t base = (uint32_t)(size_t)(lds_void_t *)slot + (uint32_t)(tid & ~63) * 16;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(base + 256 * 16 * k);
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src + 256 * k + tid), "s"(dst)
+            : "memory");
+    }
+}
+
 template <int L>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
-                  C2 *fa, C2 *fb, double2 *s_bk, const double2 *__restrict__ next_pair, bool has_next,
+                  C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
                   PhaseProf &pp) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
@@ -567,26 +588,27 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
         load_digits_lds(d[0], s_tmp, 2 * rp, L, bgbit, twist_t, t);
         load_digits_lds(d[1], s_tmp, 2 * rp + 1, L, bgbit, twist_t, t);
 #ifndef TFHE_KO_FFT  // TFHE_KO_*: development knock-out builds (timing only)
-        fft512_x2<false>(d, xb, T, t);
+        fft512_x2<false, true>(d, xb, T, t);
 #endif
         pp.mark(2);
+        const int slot = (slot0 + rp) & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the pair's DMA landed
 #ifndef TFHE_KO_BAR
-        __syncthreads();  // BK pair has landed (s_waitcnt vmcnt(0) + s_barrier)
+        // the pair is in slot `slot` for every wave, and every wave is done
+        // with the previous pair (the other slot), which the next DMA refills
+        __syncthreads();
+#endif
+        pp.mark(7);
+#ifndef TFHE_KO_DMA
+        if (rp + 1 < L || has_next) issue_bk_pair_async(next_pair + (size_t)rp * 2048, s_bk + (slot ^ 1) * 2048, tid);
 #endif
         pp.mark(3);
 #ifndef TFHE_KO_MAC
-        mac_pair_lds(fa, fb, d[0], d[1], s_bk, t);
+        mac_pair_lds(fa, fb, d[0], d[1], s_bk + slot * 2048, t);
 #else
         for (int q = 0; q < 8; q++) fa[q] = c2(fa[q].x + d[0][q].x, fa[q].y + d[1][q].y);
 #endif
         pp.mark(4);
-#ifndef TFHE_KO_BAR
-        __syncthreads();  // every wave is done reading the pair
-#endif
-        pp.mark(7);
-#ifndef TFHE_KO_DMA
-        if (rp + 1 < L || has_next) issue_bk_pair(next_pair + (size_t)rp * 2048, s_bk, tid);
-#endif
     }
 }
 
@@ -676,10 +698,10 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         }
         wave_sync();
         C2 fa[8], fb[8];
-        br_pairs<L>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, bkd + (size_t)i * step_stride + 2048,
-                    i + 1 < n, pp);
+        br_pairs<L>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
+                    bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp);
         pp.mark(5);
-        inverse_and_add<SMALL, 64>(fa, fb, s_x, T, twist_t, t, accA, accB);
+        inverse_and_add<SMALL, 64, true>(fa, fb, s_x, T, twist_t, t, accA, accB);
         wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) {
