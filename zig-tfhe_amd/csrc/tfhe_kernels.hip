@@ -680,16 +680,30 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         // tmp = X^{a~} acc - acc (+ decomposition offset), written over the
         // accumulator's LDS copy (the old acc stays in accA/accB registers)
         uint32_t tA[16], tB[16];
+#ifndef TFHE_KO_TMP
+        // all 32 gathers first (one wait), then the arithmetic: interleaved,
+        // hipcc waits for every gather before issuing the next
+        const int rb = (t - at) & 2047;
 #pragma unroll
         for (int m = 0; m < 16; m++) {
-#ifndef TFHE_KO_TMP
-            tA[m] = rot_read(s_acc, t + 64 * m, at) - accA[m] + P.offset;
-            tB[m] = rot_read(s_acc + 1024, t + 64 * m, at) - accB[m] + P.offset;
+            const int j = (rb + 64 * m) & 1023;
+            tA[m] = s_acc[j];
+            tB[m] = s_acc[1024 + j];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            const bool neg = ((rb + 64 * m) & 1024) != 0;  // X^a~ wraps past N: negacyclic sign
+            tA[m] = (neg ? 0u - tA[m] : tA[m]) - accA[m] + P.offset;
+            tB[m] = (neg ? 0u - tB[m] : tB[m]) - accB[m] + P.offset;
+        }
 #else
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
             tA[m] = accA[m] * at + P.offset;
             tB[m] = accB[m] * at + P.offset;
-#endif
         }
+#endif
         wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) {
