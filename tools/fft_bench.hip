@@ -40,7 +40,7 @@ int main() {
     for (int k = 0; k < 512; k++) h[k] = {cos(k * 0.01), -sin(k * 0.01)};
     hipMemcpy(tw, h.data(), 512 * 16, hipMemcpyHostToDevice);
     hipMemcpy(twist, h.data(), 512 * 16, hipMemcpyHostToDevice);
-    DevTables T{twist, tw};
+    DevTables T{twist, tw, {h[2], h[4], h[5], h[6]}};
     const int iters = 2000, blocks = 256;
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     const char *nm[4] = {"fft512_x2 (pair, pipelined)", "2 x fft512<1>", "passes only, no exchange", "passA + exchange only"};

@@ -37,7 +37,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(d_tv, tv.data(), 2048 * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_tw, tw.data(), 512 * 16, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_twist, twist.data(), 512 * 16, hipMemcpyHostToDevice));
-    DevTables T{d_twist, d_tw};
+    DevTables T{d_twist, d_tw, {tw[2], tw[4], tw[5], tw[6]}};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int rep = 0; rep < 2; rep++) {

@@ -30,6 +30,7 @@ struct tfhe_gpu_ctx {
     std::string err;
     // constant tables
     C2 *d_twist = nullptr, *d_tw = nullptr;
+    C2 twa[4] = {};  // host copy of the pass-A twiddles (DevTables::twa)
     // cloud key
     bool has_key = false;
     uint32_t offset = 0;
@@ -93,7 +94,9 @@ int ensure(tfhe_gpu_ctx *c, DevBuf &b, size_t bytes) {
     return TFHE_OK;
 }
 
-DevTables tables(const tfhe_gpu_ctx *c) { return DevTables{c->d_twist, c->d_tw}; }
+DevTables tables(const tfhe_gpu_ctx *c) {
+    return DevTables{c->d_twist, c->d_tw, {c->twa[0], c->twa[1], c->twa[2], c->twa[3]}};
+}
 
 size_t tlwe0_words(const tfhe_gpu_ctx *c) { return (size_t)c->P.n + 1; }
 size_t bk_rows(const tfhe_params &p) { return (size_t)p.n * 2 * p.L; }
@@ -247,6 +250,10 @@ int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
         std::vector<C2> tw2(tre.size()), st2(fre.size());
         for (size_t i = 0; i < tre.size(); i++) tw2[i] = C2{tre[i], tim[i]};
         for (size_t i = 0; i < fre.size(); i++) st2[i] = C2{fre[i], fim[i]};
+        c->twa[0] = st2[2];
+        c->twa[1] = st2[4];
+        c->twa[2] = st2[5];
+        c->twa[3] = st2[6];
         if (hipMalloc((void **)&c->d_twist, sizeof(C2) * tw2.size()) != hipSuccess ||
             hipMalloc((void **)&c->d_tw, sizeof(C2) * st2.size()) != hipSuccess) {
             rc = fail(c, TFHE_ERR_OOM, "hipMalloc(tables)");

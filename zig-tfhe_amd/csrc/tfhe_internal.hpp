@@ -44,6 +44,7 @@ enum BrOut : int {
 struct DevTables {
     const C2 *twist;  // N/2 twisting factors exp(i*pi*k/N)        fft.zig:92-106
     const C2 *tw;     // N/2-1 forward stage twiddles (recurrence)  fft.zig:590-616
+    C2 twa[4];        // tw[2], tw[4], tw[5], tw[6]: the lane-uniform pass-A twiddles, by value (SGPRs)
 };
 
 // ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------

@@ -147,6 +147,12 @@ struct LdsTw {
         a[2] = tw[5];
         a[3] = tw[6];
     }
+    // pass-A twiddles are lane-uniform: kernel-argument copies keep them in
+    // SGPRs (VALU f64 ops take one SGPR-pair operand), not 16 VGPRs
+    DEV void init(const C2 *lds_tw, const DevTables &TT) {
+        tw = lds_tw;
+        for (int k = 0; k < 4; k++) a[k] = TT.twa[k];
+    }
     DEV void pass_b(C2 *w, int t) const { tw_pass_b(w, tw, t); }
     DEV void pass_c(C2 *w, int t) const { tw_pass_c(w, tw, t); }
 };
@@ -667,7 +673,7 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     }
     __syncthreads();  // tables visible to every wave
     LdsTw T;
-    T.init(s_tw);
+    T.init(s_tw, TT);
     const C2 *twist_t = s_twist + t;  // twist of coefficient t + 64m at [64m]
     PhaseProf pp;
     pp.start();
@@ -839,7 +845,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
         s_acc[t + 64 * m] = acc[m];
     }
     LdsTw T;
-    T.init(s_tw);
+    T.init(s_tw, TT);
     const C2 *twist_t = s_twist + t;
     const C2 *spec_0 = s_xg;        // spectrum of row 2r (wave 0 of the item)
     const C2 *spec_1 = s_xg + 512;  // spectrum of row 2r+1 (wave 1)
