@@ -206,14 +206,17 @@ def main():
     ap.add_argument("--params", default="128")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--workload", default="nand", choices=["nand", "adder", "mixed", "lut"],
                     help="nand = the headline metric (default); others: BASELINE configs 3-5")
     args = ap.parse_args()
 
     rank, world, local = tdist.env_rank_world()
     if world > 1:
-        dist.init_process_group("nccl")  # RCCL
-    device = torch.device("cuda", local)
+        dist.init_process_group(args.dist_backend)  # nccl = RCCL over xGMI
+    # one rank per GPU; --dist-backend gloo with more ranks than GPUs only
+    # rehearses the multi-rank path (ranks then share a device)
+    device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
     if args.workload != "nand":
         run_workload(args, rank, world, device)
@@ -221,7 +224,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    ctx = tfhe_amd.Context(args.params, local)
+    ctx = tfhe_amd.Context(args.params, device.index)
     p = ctx.params
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     bk = ksk = None
