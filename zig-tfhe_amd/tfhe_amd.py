@@ -18,7 +18,7 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libtfhe_gpu.so")
+LIB_PATH = os.environ.get("TFHE_GPU_LIB") or os.path.join(HERE, "lib", "libtfhe_gpu.so")  # env: A/B builds
 
 # gate op codes, include/tfhe_gpu.h TFHE_GATE_* (gates.zig:48-121)
 NAND, OR, AND, XOR, XNOR, NOR, ANDNY, ANDYN, ORNY, ORYN = range(10)
