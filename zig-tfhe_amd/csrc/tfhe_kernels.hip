@@ -331,11 +331,10 @@ DEV uint32_t torus_from_f64(double v) {
 // then t + 1.5*2^52 is exact and its low mantissa word is t mod 2^32.
 DEV uint32_t torus_from_f64_small(double v) {
     const double t = trunc(v);
-    const double frac = v - t;  // exact
-    const double s = t + 6755399441055744.0;
-    const uint32_t lo = (uint32_t)__double_as_longlong(s);
-    const uint32_t adj = fabs(frac) >= 0.5 ? (v < 0.0 ? 0xFFFFFFFFu : 1u) : 0u;
-    return lo + adj;
+    const double frac = v - t;                // exact, |frac| < 1, sign of v
+    const double adj = trunc(frac + frac);    // exact: +-1 iff |frac| >= 0.5 (half away from zero), else 0
+    const double s = (t + adj) + 6755399441055744.0;  // exact integers < 2^51, then 1.5*2^52
+    return (uint32_t)__double_as_longlong(s);
 }
 
 template <bool SMALL>
