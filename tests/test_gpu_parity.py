@@ -93,10 +93,10 @@ def test_key_switch_vs_oracle(oracle, pname, B, form, monkeypatch):
 
 
 # ---- blind rotation / bootstrap ---------------------------------------------
-@pytest.mark.parametrize("form", ["whole", "split"])
+@pytest.mark.parametrize("form", ["whole", "split", "wide"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
 def test_blind_rotate_vs_oracle(oracle, pname, B, form, monkeypatch):
-    """Both kernel forms (1 wave per item / 2 waves per item) bit-exact."""
+    """All kernel forms (1 wave per item / 2 waves per item / 8 waves per item) bit-exact."""
     monkeypatch.setenv("TFHE_BR_KERNEL", form)
     c, k = ctx_for(oracle, pname)
     cts = u32rand(rng(6), B, k.p.n + 1)  # uniform TLWE: bit-exactness only
@@ -108,7 +108,7 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form, monkeypatch):
     assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
-@pytest.mark.parametrize("form", ["whole", "split"])
+@pytest.mark.parametrize("form", ["whole", "split", "wide"])
 def test_bootstrap_without_key_switch(oracle, form, monkeypatch):
     """VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69) and the
     strategy mirror: blind rotation + the hybrid sampleExtractIndex2."""

@@ -946,6 +946,141 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
 }
 
 // ---------------------------------------------------------------------------
+// Blind rotation, latency form ("wide"): ONE item per 512-thread workgroup,
+// for batches too small to give every SIMD a gate (circuit levels, single
+// gates).  Per CMUX step:
+//   waves r < 2L : row r's digits (rotation gathered from the LDS accumulator)
+//                  and forward transform, spectrum published in slot r
+//   all 8 waves  : MAC of 64 frequencies each (t + 64w) over rows 0..2L-1 in
+//                  the reference's order, BK words streamed from HBM/L2 into
+//                  registers one step ahead; products written over slots 0/1
+//   waves 0, 1   : inverse transform of polynomial w and the CMUX add
+// Same arithmetic as the other forms, bit for bit.
+// ---------------------------------------------------------------------------
+constexpr int BW_WAVES = 8;
+constexpr size_t BR_WIDE_MAX_ITEMS = 512;  // measured: 1 gate 4.3 vs 9.9 ms; 512 gates 8.8 vs 10.2 ms; 1024: 17.1 vs 10.4 ms
+
+template <int L, bool SMALL>
+__global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
+    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
+    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
+    __shared__ __attribute__((aligned(16))) C2 s_tw[512];
+    __shared__ __attribute__((aligned(16))) C2 s_twist[512];
+    __shared__ __attribute__((aligned(16))) C2 s_slot[2 * L][512];
+    __shared__ __attribute__((aligned(16))) uint32_t s_acc[2048];
+    __shared__ uint16_t s_at[1024];
+    __shared__ int s_bt;
+    const int tid = threadIdx.x;
+    const int t = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n = P.n;
+    const size_t g = blockIdx.x;
+    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
+    const uint32_t *A = in_a + ia * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
+    const int op = ops ? (int)ops[g] : 255;
+    const size_t trgsw = (size_t)2 * L * 1024;  // double2 per BK[i]
+
+    for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
+    if (w == 0) {
+        for (int i = t; i <= n; i += 64) {
+            uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
+            uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
+            if (i < n) s_at[i] = (uint16_t)tl;
+            else s_bt = 2048 - (int)tl;
+        }
+    }
+    // this wave's BK words of step 0: rows r, parts a|b, frequency t + 64w
+    double2 kb[2 * L][2];
+#pragma unroll
+    for (int r = 0; r < 2 * L; r++)
+#pragma unroll
+        for (int h = 0; h < 2; h++) kb[r][h] = bkd[((size_t)r * 8 + w) * 128 + h * 64 + t];
+    __syncthreads();
+    const int bt = __builtin_amdgcn_readfirstlane(s_bt);
+    if (w < 2) {
+#pragma unroll
+        for (int m = 0; m < 16; m++) s_acc[w * 1024 + t + 64 * m] = rot_read(testvec + w * 1024, t + 64 * m, bt);
+    }
+    LdsTw T;
+    T.init(s_tw, TT);
+    const C2 *twist_t = s_twist + t;
+    __syncthreads();
+
+    for (int i = 0; i < n; i++) {
+        const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
+        if (w < 2 * L) {
+            const int poly = w >= L ? 1 : 0;
+            const int level = w - poly * L;
+            const uint32_t *pa = s_acc + poly * 1024;
+            C2 d[1][8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int m = br3(q);
+                const int c0 = t + 64 * m, c1 = c0 + 512;
+                const uint32_t x0 = rot_read(pa, c0, at) - pa[c0] + P.offset;
+                const uint32_t x1 = rot_read(pa, c1, at) - pa[c1] + P.offset;
+                d[0][q] = twist_in(digit_f64(x0, level, P.bgbit), digit_f64(x1, level, P.bgbit), twist_t[64 * m]);
+            }
+            fft512<1, false>(d, s_slot[w], T, t);
+#pragma unroll
+            for (int q = 0; q < 8; q++) s_slot[w][t + 64 * q] = d[0][q];  // publish (after this wave's exchanges)
+        }
+        __syncthreads();  // every row's spectrum is in its slot
+        const int f = t + 64 * w;
+        C2 fa = c2(0.0, 0.0), fb = c2(0.0, 0.0);  // fmaInFd1024 accumulates from 0.0
+#pragma unroll
+        for (int r = 0; r < 2 * L; r++) {
+            const C2 x = s_slot[r][f];
+            const C2 ta = cmul_bk(x, kb[r][0]);
+            const C2 tb = cmul_bk(x, kb[r][1]);
+            fa = c2(fa.x + ta.x, fa.y + ta.y);
+            fb = c2(fb.x + tb.x, fb.y + tb.y);
+        }
+        if (i + 1 < n) {  // next step's BK words, landing under the inverse and forward phases
+            const double2 *nb = bkd + (size_t)(i + 1) * trgsw;
+#pragma unroll
+            for (int r = 0; r < 2 * L; r++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) kb[r][h] = nb[((size_t)r * 8 + w) * 128 + h * 64 + t];
+        }
+        // frequency f of slots 0/1 is read and rewritten by this lane only
+        s_slot[0][f] = fa;
+        s_slot[1][f] = fb;
+        __syncthreads();  // both product spectra complete
+        if (w < 2) {
+            C2 e[1][8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) e[0][q] = s_slot[w][t + 64 * br3(q)];
+            fft512<1, true>(e, s_slot[w], T, t);
+            uint32_t *pa = s_acc + w * 1024;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                double re, im;
+                untwist_out(e[0][q], twist_t[64 * q], re, im);
+                pa[t + 64 * q] += to_torus<SMALL>(re);
+                pa[t + 64 * q + 512] += to_torus<SMALL>(im);
+            }
+        }
+        __syncthreads();  // accumulator updated
+    }
+
+    if (w != 0) return;
+    if (out_mode == BR_OUT_LV1) {
+        uint32_t *o = out + g * (size_t)1025;
+        for (int j = t; j <= 1024; j += 64) o[j] = j == 0 ? s_acc[0] : j < 1024 ? 0u - s_acc[1024 - j] : s_acc[1024];
+    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {
+        uint32_t *o = out + g * (size_t)(n + 1);
+        for (int j = t; j <= n; j += 64) o[j] = j == 0 ? s_acc[0] : j < n ? 0u - s_acc[n - j] : s_acc[1024];
+    } else {
+        uint32_t *o = out + g * (size_t)2048;
+        for (int j = t; j < 2048; j += 64) o[j] = s_acc[j];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Identity key switching (trgsw.zig:471-502):
 //   res = (0,...,0, b) - sum_{i<N, j<t} KSK[i][j][digit_j(a_i + 2^(32-(1+basebit*t)))]
 // Integer gather-subtract; the k = 0 rows of the device KSK are zero (the
@@ -1378,12 +1513,18 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     // |external product| <= 2L * N * Bg/2 * 2^31: the 8-op exact conversion
     // needs it below 2^51 (true for the L=3 / Bg=2^6 sets, false for UINT4)
     const bool small = std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 50);
-    // kernel form: whole (1 wave per item, default: measured faster) or split
-    // (2 waves per item); knob TFHE_BR_KERNEL=whole|split for A/B runs and tests
+    // kernel form: wide (8 waves per item) for batches up to BR_WIDE_MAX_ITEMS,
+    // else whole (1 wave per item); split (2 waves per item) on request.
+    // Knob TFHE_BR_KERNEL=whole|split|wide forces a form (A/B runs and tests).
     const char *form = getenv("TFHE_BR_KERNEL");
     const bool split = form && form[0] == 's';
+    // latency form for batches below one gate per SIMD pair (TFHE_BR_KERNEL=wide forces it)
+    const bool wide = form ? form[0] == 'W' || (form[0] == 'w' && form[1] == 'i') : B <= BR_WIDE_MAX_ITEMS;
     dim3 grid, block;
-    if (split) {
+    if (wide) {
+        grid = dim3((unsigned)B);
+        block = dim3(64 * BW_WAVES);
+    } else if (split) {
         grid = dim3((unsigned)((B + BS_GATES - 1) / BS_GATES));
         block = dim3(64 * BS_WAVES);
     } else {
@@ -1392,7 +1533,10 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     }
 #define BR_LAUNCH(L_, S_)                                                                                         \
     do {                                                                                                          \
-        if (split)                                                                                                \
+        if (wide)                                                                                                 \
+            hipLaunchKernelGGL((k_blind_rotate_wide<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,      \
+                               testvec, bk2, out, out_mode, B);                                                   \
+        else if (split)                                                                                           \
             hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
                                testvec, bk2, out, out_mode, B);                                                   \
         else                                                                                                      \
