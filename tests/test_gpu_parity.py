@@ -182,6 +182,35 @@ def test_nand_batch_1024_128bit(oracle):
     assert np.array_equal(c.gate_batch(np.zeros(64, np.uint8), A[:64], B[:64]), out[:64])
 
 
+TRUTH = {0: lambda a, b: ~(a & b), 1: lambda a, b: a | b, 2: lambda a, b: a & b, 3: lambda a, b: a ^ b,
+         4: lambda a, b: a ^ b,  # reference xnorGate computes a - 2b + 1/4: decrypts as XOR (test_oracle.py)
+         5: lambda a, b: ~(a | b), 6: lambda a, b: ~a & b, 7: lambda a, b: a & ~b, 8: lambda a, b: ~a | b,
+         9: lambda a, b: a | ~b}
+
+
+def test_all_ops_ragged_batch_1027_128bit(oracle):
+    """Full-size mixed batch, 1027 gates (ragged last workgroup, whole form): every
+    gate's truth table, a bit-exact sample vs the oracle, and the first 300 again
+    through the latency form (B <= 512) — the two forms agree bit for bit."""
+    c, k = ctx_for(oracle, "128")
+    p = k.p
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    g = rng(19)
+    B = 1027
+    ops = g.integers(0, 10, B).astype(np.uint8)
+    a_bits = g.integers(0, 2, B).astype(bool)
+    b_bits = g.integers(0, 2, B).astype(bool)
+    A = sk.encrypt_bool(a_bits.astype(np.uint8), seed0=30_000)
+    Bc = sk.encrypt_bool(b_bits.astype(np.uint8), seed0=40_000)
+    out = c.gate_batch(ops, A, Bc)
+    want_bits = np.array([TRUTH[int(o)](x, y) for o, x, y in zip(ops, a_bits, b_bits)], bool)
+    assert np.array_equal(sk.decrypt_bool(out), want_bits)
+    idx = np.concatenate([g.choice(B - 3, 5, replace=False), [B - 3, B - 2, B - 1]])
+    want = oracle.gate_batch(p, ops[idx], A[idx], Bc[idx], k.ck, threads=8)
+    assert np.array_equal(out[idx], want)
+    assert np.array_equal(c.gate_batch(ops[:300], A[:300], Bc[:300]), out[:300])
+
+
 def test_lut_pbs_uint4(oracle):
     """BASELINE config 5 semantics: f(x) = (x+1) mod 16 over all 16 messages."""
     c, k = ctx_for(oracle, "uint4")
