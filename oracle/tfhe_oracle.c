@@ -367,7 +367,7 @@ void oracle_external_product(const oracle_params *p, const double *trgsw_fft,
 void oracle_cmux(const oracle_params *p, const uint32_t *in1, const uint32_t *in2,
                  const double *trgsw_fft, uint32_t offset, uint32_t *out) {
     uint32_t N = p->N;
-    uint32_t *tmp = (uint32_t *)malloc(sizeof(uint32_t) * 2 * N);
+    uint32_t *tmp = (uint32_t *)calloc(2 * N, sizeof(uint32_t));
     uint32_t *tmp2 = (uint32_t *)malloc(sizeof(uint32_t) * 2 * N);
     for (uint32_t i = 0; i < 2 * N; i++) tmp[i] = in2[i] - in1[i]; /* rot - acc */
     oracle_external_product(p, trgsw_fft, tmp, offset, tmp2);
