@@ -552,8 +552,13 @@ DEV void load_digits_lds(C2 *d, const uint32_t *s_tmp, int row, int L, int bgbit
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         const int m = br3(q);
+#ifndef TFHE_KO_DIG
         d[q] = twist_in(digit_f64(src[64 * m], level, bgbit), digit_f64(src[64 * (m + 8)], level, bgbit),
                         twist_t[64 * m]);
+#else
+        d[q] = twist_in(digit_f64((uint32_t)(t * 77 + q), level, bgbit), digit_f64((uint32_t)(t * 5 + m), level, bgbit),
+                        twist_t[64 * m]);
+#endif
     }
 }
 
