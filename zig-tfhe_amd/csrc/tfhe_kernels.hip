@@ -681,12 +681,13 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     const C2 *twist_t = s_twist + t;  // twist of coefficient t + 64m at [64m]
     PhaseProf pp;
     pp.start();
+    int at_next = s_at[0];  // a~ of the coming step, read one step ahead
 
     for (int i = 0; i < n; i++) {
         pp.mark(0);
         // a~ in {0, 2N} gives tmp = 0 and an exactly-zero external product;
         // it is computed anyway so the four waves keep one barrier schedule.
-        const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
+        const int at = __builtin_amdgcn_readfirstlane(at_next);
         // tmp = X^{a~} acc - acc (+ decomposition offset), written over the
         // accumulator's LDS copy (the old acc stays in accA/accB registers)
         uint32_t tA[16], tB[16];
@@ -722,6 +723,7 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         }
         wave_sync();
         C2 fa[8], fb[8];
+        at_next = s_at[i + 1 < n ? i + 1 : i];
         br_pairs<L>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
                     bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp);
         pp.mark(5);
