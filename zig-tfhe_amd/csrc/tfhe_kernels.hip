@@ -562,6 +562,28 @@ DEV void load_digits_lds(C2 *d, const uint32_t *s_tmp, int row, int L, int bgbit
     }
 }
 
+// Digits of rows (row, row+1) with one read of the 8 twist factors for both.
+DEV void load_digits_pair_lds(C2 (*d)[8], const uint32_t *s_tmp, int row, int L, int bgbit, const C2 *twist_t,
+                              int t) {
+    const uint32_t *src[2];
+    int level[2];
+#pragma unroll
+    for (int f = 0; f < 2; f++) {
+        const bool from_a = row + f < L;
+        src[f] = s_tmp + (from_a ? 0 : 1024) + t;
+        level[f] = from_a ? row + f : row + f - L;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int m = br3(q);
+        const C2 w = twist_t[64 * m];
+#pragma unroll
+        for (int f = 0; f < 2; f++)
+            d[f][q] = twist_in(digit_f64(src[f][64 * m], level[f], bgbit), digit_f64(src[f][64 * (m + 8)], level[f], bgbit),
+                               w);
+    }
+}
+
 // Row pairs of one CMUX step: forward FFTs of rows (2rp, 2rp+1), wait for the
 // pair's BK rows in LDS, MAC, release the buffer and prefetch the next pair.
 // LDS-DMA of one BK row pair (32 KB) into a slot, 8 x 16 B per thread, in
@@ -595,8 +617,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
     for (int rp = 0; rp < L; rp++) {
         C2 d[2][8];
         pp.mark(1);
-        load_digits_lds(d[0], s_tmp, 2 * rp, L, bgbit, twist_t, t);
-        load_digits_lds(d[1], s_tmp, 2 * rp + 1, L, bgbit, twist_t, t);
+        load_digits_pair_lds(d, s_tmp, 2 * rp, L, bgbit, twist_t, t);
 #ifndef TFHE_KO_FFT  // TFHE_KO_*: development knock-out builds (timing only)
         fft512_x2<false, true>(d, xb, T, t);
 #endif
