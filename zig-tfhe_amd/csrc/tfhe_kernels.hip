@@ -1037,19 +1037,30 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     const C2 *twist_t = s_twist + t;
     __syncthreads();
 
+    int at_next = s_at[0];  // a~ read one step ahead (its wait would drain every LDS op)
     for (int i = 0; i < n; i++) {
-        const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
+        const int at = __builtin_amdgcn_readfirstlane(at_next);
+        at_next = s_at[i + 1 < n ? i + 1 : i];
         if (w < 2 * L) {
             const int poly = w >= L ? 1 : 0;
             const int level = w - poly * L;
             const uint32_t *pa = s_acc + poly * 1024;
+            // gathers and own words first, arithmetic after (one wait)
+            uint32_t rot[16], own[16];
+            const int rb = (t - at) & 2047;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                rot[m] = pa[(rb + 64 * m) & 1023];
+                own[m] = pa[t + 64 * m];
+            }
+            __builtin_amdgcn_sched_barrier(0);
             C2 d[1][8];
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int m = br3(q);
-                const int c0 = t + 64 * m, c1 = c0 + 512;
-                const uint32_t x0 = rot_read(pa, c0, at) - pa[c0] + P.offset;
-                const uint32_t x1 = rot_read(pa, c1, at) - pa[c1] + P.offset;
+                const bool n0 = ((rb + 64 * m) & 1024) != 0, n1 = ((rb + 64 * (m + 8)) & 1024) != 0;
+                const uint32_t x0 = (n0 ? 0u - rot[m] : rot[m]) - own[m] + P.offset;
+                const uint32_t x1 = (n1 ? 0u - rot[m + 8] : rot[m + 8]) - own[m + 8] + P.offset;
                 d[0][q] = twist_in(digit_f64(x0, level, P.bgbit), digit_f64(x1, level, P.bgbit), twist_t[64 * m]);
             }
             fft512<1, false>(d, s_slot[w], T, t);
