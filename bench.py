@@ -13,7 +13,8 @@ Other BASELINE configs (parity cases; these print their own line, never the
 default one): --workload adder (config 3: 16-bit ripple-carry adder, one
 circuit = 80 gates in 33 levels, and --batch independent adders side by side),
 mixed (config 4: --batch gates per GPU, op uniform over AND/OR/XOR/MUX),
-lut (config 5: UINT4 programmable bootstrap, --batch 4096).
+lut (config 5: UINT4 programmable bootstrap, --batch 4096), reenc (SURVEY
+§8f N4: proxy re-encryption of --batch TLWELv0 ciphertexts).
 """
 from __future__ import annotations
 
@@ -175,6 +176,21 @@ def run_workload(args, rank, world, device):
         extra = {"bootstraps_per_sec": round(n_boot * world * args.steps / el, 2), "levels": depth,
                  "decrypt_check": ok}
         workload = f"{B} gates per GPU, op uniform over AND/OR/XOR/MUX (MUX = 3 bootstraps, 2 levels)"
+    elif args.workload == "reenc":
+        B = args.batch
+        alice, bob = tfhe_amd.secret_key_new(p, 11), tfhe_amd.secret_key_new(p, 12)
+        key = tfhe_amd.ProxyReencryptionKey.new_symmetric(alice, bob, 1000)  # same seeds on every rank
+        hr = tfhe_amd.HipReencryptor(ctx, key)
+        bits = g.integers(0, 2, B).astype(np.uint8)
+        cts = alice.encrypt_bool(bits, seed0=1)
+        el, outs = timed(lambda: hr.reencrypt(cts), args.steps, args.warmup, world, device)
+        ok = bool(np.array_equal(bob.decrypt_bool(outs), bits.astype(bool)))
+        hr.close()
+        units = B * world * args.steps
+        metric, unit = "TLWELv0 proxy re-encryptions/sec", "reencryptions/s"
+        extra = {"decrypt_check": ok, "dtype": "u32"}
+        workload = (f"{B} reencryptTLWELv0 per GPU (proxy_reenc.zig:267-306; n={p.n}, basebit {p.basebit}, "
+                    f"t={p.iks_t}; host buffers, PCIe included)")
     else:  # lut
         B = args.batch
         m = 16
@@ -207,7 +223,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
-    ap.add_argument("--workload", default="nand", choices=["nand", "adder", "mixed", "lut"],
+    ap.add_argument("--workload", default="nand", choices=["nand", "adder", "mixed", "lut", "reenc"],
                     help="nand = the headline metric (default); others: BASELINE configs 3-5")
     args = ap.parse_args()
 

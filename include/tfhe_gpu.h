@@ -132,6 +132,18 @@ int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *in
                           const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
                           const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels);
 
+/* ---- Proxy re-encryption (proxy_reenc.zig) -------------
+ * reencryptTLWELv0 is the identity key switch over a TLWELv0 input (n
+ * coefficients instead of N), so it runs on the same lane-per-item kernel.
+ * The key is ProxyReencryptionKey.key_encryptions: n*t*2^basebit TLWELv0 at
+ * index (2^basebit*t*i) + (2^basebit*j) + k (proxy_reenc.zig:150-196). */
+typedef struct tfhe_gpu_reenc_key tfhe_gpu_reenc_key;
+int  tfhe_gpu_reenc_key_load(tfhe_gpu_ctx *ctx, const uint32_t *key_encryptions, size_t len /* words */,
+                             uint32_t basebit, uint32_t t, tfhe_gpu_reenc_key **out);
+void tfhe_gpu_reenc_key_destroy(tfhe_gpu_reenc_key *key);
+int  tfhe_gpu_reencrypt_batch(tfhe_gpu_ctx *ctx, const tfhe_gpu_reenc_key *key, const uint32_t *in,
+                              uint32_t *out, size_t B);
+
 /* ---- Same, on device-resident buffers (async on the context stream) ---- */
 int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *ctx, const uint8_t *ops_dev, const uint32_t *a_dev,
                             const uint32_t *b_dev, uint32_t *out_dev, size_t B);
@@ -162,6 +174,8 @@ int tfhe_gpu_external_product_batch(tfhe_gpu_ctx *ctx, const double *trgsw_fft, 
 int tfhe_gpu_key_switch_batch(tfhe_gpu_ctx *ctx, const uint32_t *in_lv1, uint32_t *out_lv0, size_t B);
 
 /* ---- Host-side TLWELv0 helpers (no device needed) ---------------------- */
+/* SecretKey.new (key.zig:41-57) from DefaultPrng(seed): n lv0 bits, then N lv1 bits. */
+int tfhe_secret_key_new(const tfhe_params *params, uint64_t seed, uint32_t *key_lv0, uint32_t *key_lv1);
 /* TLWELv0.encryptBool (tlwe.zig:52-55 -> encryptF64 :34-49); item i uses
  * DefaultPrng(seed0 + i) in place of getUniqueSeed(). */
 int tfhe_encrypt_bool_batch(const tfhe_params *params, const uint32_t *key_lv0, const uint8_t *bits,
@@ -175,6 +189,22 @@ int tfhe_encrypt_lwe_message_batch(const tfhe_params *params, const uint32_t *ke
                                    size_t B);
 int tfhe_decrypt_lwe_message_batch(const tfhe_params *params, const uint32_t *key_lv0,
                                    const uint32_t *ct, uint32_t m, uint32_t *msgs, size_t B);
+/* Proxy re-encryption key material (host, seeded; the reference's
+ * getUniqueSeed() for the k-th encryptF64 call of a routine becomes seed0 + k).
+ * PublicKeyLv0.newWithParams (proxy_reenc.zig:57-76): `size` encryptions of 0. */
+int tfhe_public_key_gen(const tfhe_params *params, const uint32_t *key_lv0, size_t size, double alpha,
+                        uint64_t seed0, uint32_t *pk /* size*(n+1) */);
+/* PublicKeyLv0.encryptBool (proxy_reenc.zig:83-120), one DefaultPrng(seed0 + i) per item. */
+int tfhe_public_key_encrypt_bool_batch(const tfhe_params *params, const uint32_t *pk, size_t pk_size,
+                                       const uint8_t *bits, double alpha, uint64_t seed0, uint32_t *out,
+                                       size_t B);
+/* ProxyReencryptionKey.newSymmetricWithParams (:214-256) / newAsymmetricWithParams
+ * (:150-196); out: n*t*2^basebit*(n+1) words, k = 0 entries zero. */
+int tfhe_reenc_key_gen_symmetric(const tfhe_params *params, const uint32_t *key_from, const uint32_t *key_to,
+                                 double alpha, uint32_t basebit, uint32_t t, uint64_t seed0, uint32_t *out);
+int tfhe_reenc_key_gen_asymmetric(const tfhe_params *params, const uint32_t *key_from, const uint32_t *pk,
+                                  size_t pk_size, double alpha, uint32_t basebit, uint32_t t, uint64_t seed0,
+                                  uint32_t *out);
 /* Generator.generateLookupTableAssign (lut/generator.zig:85-135): testvec
  * (2N words, a = 0) for f given as a table f_table[x], x < m. */
 int tfhe_lut_generate(const tfhe_params *params, uint32_t m, const uint32_t *f_table,

@@ -80,6 +80,12 @@ class Oracle:
         L.oracle_cloud_key_new.argtypes = [C.c_void_p, C.c_uint64, u32p, u32p, u32p, f64p]
         L.oracle_gate_batch.argtypes = [C.c_void_p, C.c_int, C.c_size_t, u8p, u32p, u32p, u32p, f64p,
                                         u32p, C.c_uint32, u32p]
+        L.oracle_reencrypt.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p, u32p]
+        L.oracle_public_key_gen.argtypes = [C.c_uint32, u32p, C.c_size_t, C.c_double, C.c_uint64, u32p]
+        L.oracle_public_key_encrypt_f64.argtypes = [C.c_uint32, u32p, C.c_size_t, C.c_double, C.c_double,
+                                                    C.c_uint64, u32p]
+        L.oracle_reenc_key_gen.argtypes = [C.c_uint32, u32p, u32p, u32p, C.c_size_t, C.c_double, C.c_uint32,
+                                           C.c_uint32, C.c_uint64, u32p]
 
     # ---- utils / fft
     def f64_to_torus(self, d: float) -> int:
@@ -279,6 +285,34 @@ class Oracle:
         ct = np.ascontiguousarray(ct, dtype=np.uint32)
         return self.lib.oracle_tlwe_decrypt_lwe_message(C.c_uint32(n), _ptr(ct, u32p), C.c_uint32(m),
                                                         _ptr(key, u32p))
+
+    # ---- proxy re-encryption (proxy_reenc.zig)
+    def reencrypt(self, n, basebit, t, ct, key):
+        ct = np.ascontiguousarray(ct, dtype=np.uint32)
+        out = np.zeros(n + 1, dtype=np.uint32)
+        self.lib.oracle_reencrypt(n, basebit, t, _ptr(ct, u32p), _ptr(key, u32p), _ptr(out, u32p))
+        return out
+
+    def public_key_gen(self, n, key, size, alpha, seed0):
+        pk = np.zeros((size, n + 1), dtype=np.uint32)
+        self.lib.oracle_public_key_gen(n, _ptr(key, u32p), size, alpha, seed0, _ptr(pk, u32p))
+        return pk
+
+    def public_key_encrypt_f64(self, n, pk, plaintext, alpha, seed):
+        out = np.zeros(n + 1, dtype=np.uint32)
+        self.lib.oracle_public_key_encrypt_f64(n, _ptr(pk, u32p), pk.shape[0], plaintext, alpha, seed,
+                                               _ptr(out, u32p))
+        return out
+
+    def reenc_key_gen(self, n, key_from, alpha, basebit, t, seed0, key_to=None, pk=None):
+        """symmetric when key_to is given, asymmetric (public key) when pk is given"""
+        assert (key_to is None) != (pk is None)
+        out = np.zeros(((1 << basebit) * t * n, n + 1), dtype=np.uint32)
+        self.lib.oracle_reenc_key_gen(n, _ptr(key_from, u32p), None if key_to is None else _ptr(key_to, u32p),
+                                      None if pk is None else _ptr(pk, u32p),
+                                      0 if pk is None else pk.shape[0], alpha, basebit, t, seed0,
+                                      _ptr(out, u32p))
+        return out
 
 
 class CloudKeyArrays:

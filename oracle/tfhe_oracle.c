@@ -684,3 +684,64 @@ uint32_t oracle_tlwe_decrypt_lwe_message(uint32_t n, const uint32_t *ct, uint32_
     uint64_t msg = (uint64_t)(f / scale + 0.5);
     return (uint32_t)(msg % m);
 }
+
+/* ---- proxy re-encryption — proxy_reenc.zig -------------------------------- */
+
+/* reencryptTLWELv0 — proxy_reenc.zig:267-306: the identity key switch with an
+ * n-coefficient input and the re-encryption key in place of the KSK. */
+void oracle_reencrypt(uint32_t n, uint32_t basebit, uint32_t t, const uint32_t *ct, const uint32_t *key,
+                      uint32_t *out) {
+    uint32_t base = 1u << basebit;
+    for (uint32_t x = 0; x < n; x++) out[x] = 0;
+    out[n] = ct[n];
+    uint32_t prec_offset = 1u << (32 - (1 + basebit * t));
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t a_bar = ct[i] + prec_offset;
+        for (uint32_t j = 0; j < t; j++) {
+            uint32_t k = (a_bar >> (32 - (j + 1) * basebit)) & (base - 1);
+            if (k == 0) continue;
+            const uint32_t *row = key + ((size_t)base * t * i + (size_t)base * j + k) * (n + 1);
+            for (uint32_t x = 0; x <= n; x++) out[x] -= row[x];
+        }
+    }
+}
+
+/* PublicKeyLv0.newWithParams — proxy_reenc.zig:57-76 */
+void oracle_public_key_gen(uint32_t n, const uint32_t *key, size_t size, double alpha, uint64_t seed0,
+                           uint32_t *pk) {
+    for (size_t e = 0; e < size; e++) oracle_tlwe_encrypt_f64(n, 0.0, alpha, key, seed0 + e, pk + e * (n + 1));
+}
+
+/* PublicKeyLv0.encryptF64 — proxy_reenc.zig:83-113 */
+void oracle_public_key_encrypt_f64(uint32_t n, const uint32_t *pk, size_t size, double plaintext, double alpha,
+                                   uint64_t seed, uint32_t *out) {
+    oracle_rng r;
+    oracle_rng_init(&r, seed);
+    for (uint32_t x = 0; x <= n; x++) out[x] = 0;
+    out[n] = oracle_f64_to_torus(plaintext);
+    for (size_t e = 0; e < size; e++) {
+        if (!oracle_rng_bool(&r)) continue;           /* keep this encryption of zero? */
+        const uint32_t *enc = pk + e * (n + 1);
+        if (oracle_rng_bool(&r)) { for (uint32_t x = 0; x <= n; x++) out[x] += enc[x]; }
+        else                     { for (uint32_t x = 0; x <= n; x++) out[x] -= enc[x]; }
+    }
+    normal_dist nd = {0.0, alpha, 0, 0.0};
+    out[n] += gaussian_torus(0u, &nd, &r);            /* gaussianF64(0.0, ...) */
+}
+
+/* ProxyReencryptionKey.newAsymmetricWithParams :150-196 / newSymmetricWithParams :214-256 */
+void oracle_reenc_key_gen(uint32_t n, const uint32_t *key_from, const uint32_t *key_to, const uint32_t *pk,
+                          size_t pk_size, double alpha, uint32_t basebit, uint32_t t, uint64_t seed0,
+                          uint32_t *out) {
+    uint32_t base = 1u << basebit;
+    memset(out, 0, sizeof(uint32_t) * (size_t)n * t * base * (n + 1));
+    uint64_t c = 0;
+    for (uint32_t i = 0; i < n; i++)
+        for (uint32_t j = 0; j < t; j++)
+            for (uint32_t k = 1; k < base; k++) {
+                double pv = ((double)k * (double)key_from[i]) / (double)(1u << ((j + 1) * basebit));
+                uint32_t *row = out + ((size_t)base * t * i + (size_t)base * j + k) * (n + 1);
+                if (pk) oracle_public_key_encrypt_f64(n, pk, pk_size, pv, alpha, seed0 + c++, row);
+                else    oracle_tlwe_encrypt_f64(n, pv, alpha, key_to, seed0 + c++, row);
+            }
+}

@@ -120,6 +120,22 @@ void oracle_tlwe_encrypt_lwe_message(uint32_t n, uint32_t msg, uint32_t m, doubl
                                      const uint32_t *key, uint64_t seed, uint32_t *out);
 uint32_t oracle_tlwe_decrypt_lwe_message(uint32_t n, const uint32_t *ct, uint32_t m, const uint32_t *key);
 
+/* ---- proxy re-encryption (proxy_reenc.zig) -------------------------- */
+/* reencryptTLWELv0 :267-306 — key: n*t*2^basebit rows of n+1 words */
+void oracle_reencrypt(uint32_t n, uint32_t basebit, uint32_t t, const uint32_t *ct /*n+1*/,
+                      const uint32_t *key, uint32_t *out /*n+1*/);
+/* PublicKeyLv0.newWithParams :57-76 — encryption e uses seed seed0+e */
+void oracle_public_key_gen(uint32_t n, const uint32_t *key, size_t size, double alpha, uint64_t seed0,
+                           uint32_t *pk /*size*(n+1)*/);
+/* PublicKeyLv0.encryptF64 :83-113 */
+void oracle_public_key_encrypt_f64(uint32_t n, const uint32_t *pk, size_t size, double plaintext, double alpha,
+                                   uint64_t seed, uint32_t *out /*n+1*/);
+/* ProxyReencryptionKey.new{Symmetric,Asymmetric}WithParams :150-256; pk == NULL selects the
+ * symmetric form (key_to used); the c-th encryption in (i, j, k) order uses seed0+c */
+void oracle_reenc_key_gen(uint32_t n, const uint32_t *key_from, const uint32_t *key_to, const uint32_t *pk,
+                          size_t pk_size, double alpha, uint32_t basebit, uint32_t t, uint64_t seed0,
+                          uint32_t *out);
+
 #ifdef __cplusplus
 }
 #endif

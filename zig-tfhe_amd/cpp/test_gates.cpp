@@ -2,7 +2,8 @@
 // reference's own gate tests are (src/gates.zig:374-544: each gate's truth
 // table through encryptBool -> gate -> decryptBool, 128-bit parameters), plus
 // muxNaive, notGate / copy / constant, the bootstrap strategy, the batch
-// functions gates.zig:244-299 declares, and a level-scheduled circuit.
+// functions gates.zig:244-299 declares, a level-scheduled circuit, and the
+// proxy re-encryption tests of src/proxy_reenc.zig:310-455.
 // Runs on one MI355X; exit status 0 = all passed.
 #include "tfhe.hpp"
 
@@ -111,6 +112,33 @@ int main() {
         expect(v == 706, "add_two_numbers circuit", "402 + 304");
         expect(levels == 33, "add_two_numbers circuit", "depth");
         std::printf("ok   add_two_numbers circuit (402 + 304 = %u, %u levels)\n", v, levels);
+    }
+    {  // proxy_reenc.zig:310-455: public key, symmetric, asymmetric, chain alice -> bob -> carol
+        const tfhe_params p = params::SECURITY_128_BIT();
+        const SecretKey alice = SecretKey::newWithSeed(p, 11), bob = SecretKey::newWithSeed(p, 12),
+                        carol = SecretKey::newWithSeed(p, 13);
+        const PublicKeyLv0 bob_pk = PublicKeyLv0::create(bob, 100000), carol_pk = PublicKeyLv0::create(carol, 200000);
+        for (bool m : {true, false})
+            expect(bob.decryptBool(bob_pk.encryptBool(m, p.alpha_lv0, 7 + m)) == m, "public key encryption", "bit");
+        const HipReencryptor sym(p, ProxyReencryptionKey::newSymmetric(alice, bob, 5));
+        const HipReencryptor ab(p, ProxyReencryptionKey::newAsymmetric(alice, bob_pk, 1000000));
+        const HipReencryptor bc(p, ProxyReencryptionKey::newAsymmetric(bob, carol_pk, 3000000));
+        for (bool m : {true, false}) {
+            const TLWELv0 ct = alice.encryptBool(m, 50 + m);
+            expect(bob.decryptBool(sym.reencryptTLWELv0(ct)) == m, "proxy reencryption symmetric", "bit");
+            expect(bob.decryptBool(ab.reencryptTLWELv0(ct)) == m, "proxy reencryption asymmetric", "bit");
+        }
+        std::vector<TLWELv0> batch;
+        std::vector<bool> bits;
+        for (int k = 0; k < 100; k++) {
+            bits.push_back((k * 2654435761u >> 7) & 1);
+            batch.push_back(alice.encryptBool(bits.back(), 600 + k));
+        }
+        const auto carol_cts = bc.reencryptBatch(ab.reencryptBatch(batch));
+        int ok = 0;
+        for (int k = 0; k < 100; k++) ok += carol.decryptBool(carol_cts[k]) == bits[k];
+        expect(ok >= 90, "proxy reencryption chain asymmetric", "accuracy");
+        std::printf("ok   proxy reencryption (symmetric, asymmetric, chain: %d/100)\n", ok);
     }
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
     return failures ? 1 : 0;

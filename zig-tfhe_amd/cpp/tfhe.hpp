@@ -7,6 +7,8 @@
 //   bootstrap.zig     -> tfhe::HipBootstrap (bootstrap / bootstrapWithoutKeySwitch / name)
 //   gates.zig Gates   -> tfhe::Gates (nandGate ... orYnGate, muxNaive, notGate, copy, constant,
 //                        batchNand ... batchXnor — placeholders in the reference, implemented here)
+//   proxy_reenc.zig   -> tfhe::PublicKeyLv0, tfhe::ProxyReencryptionKey, tfhe::HipReencryptor
+//                        (reencryptTLWELv0 on the GPU)
 // Zig error unions become tfhe::Error exceptions carrying the C status.
 // There is no CPU path: every bootstrap runs on the GPU through the C ABI.
 #pragma once
@@ -105,6 +107,82 @@ struct SecretKey {
         check(tfhe_decrypt_lwe_message_batch(&params, key_lv0.data(), ct.p.data(), m, &v, 1), "decryptLweMessage");
         return v;
     }
+    // SecretKey.new (key.zig:41-57) from DefaultPrng(seed)
+    static SecretKey newWithSeed(const tfhe_params &p, uint64_t seed) {
+        SecretKey sk;
+        sk.params = p;
+        sk.key_lv0.assign(p.n, 0u);
+        sk.key_lv1.assign(p.N, 0u);
+        check(tfhe_secret_key_new(&p, seed, sk.key_lv0.data(), sk.key_lv1.data()), "SecretKey.new");
+        return sk;
+    }
+};
+
+// proxy_reenc.zig:35-121.  Encryption e of newWithParams uses DefaultPrng(seed0 + e).
+struct PublicKeyLv0 {
+    tfhe_params params{};
+    size_t size = 0;
+    std::vector<Torus> encryptions;  // size x (n+1)
+
+    static PublicKeyLv0 newWithParams(const SecretKey &sk, size_t size, double alpha, uint64_t seed0) {
+        PublicKeyLv0 pk;
+        pk.params = sk.params;
+        pk.size = size;
+        pk.encryptions.assign(size * (sk.params.n + 1), 0u);
+        check(tfhe_public_key_gen(&sk.params, sk.key_lv0.data(), size, alpha, seed0, pk.encryptions.data()),
+              "PublicKeyLv0.new");
+        return pk;
+    }
+    static PublicKeyLv0 create(const SecretKey &sk, uint64_t seed0) {  // PublicKeyLv0.new: 2n, tlwe_lv0.ALPHA
+        return newWithParams(sk, 2 * (size_t)sk.params.n, sk.params.alpha_lv0, seed0);
+    }
+    TLWELv0 encryptBool(bool bit, double alpha, uint64_t seed) const {  // :116-120
+        TLWELv0 ct(params.n);
+        const uint8_t v = bit ? 1 : 0;
+        check(tfhe_public_key_encrypt_bool_batch(&params, encryptions.data(), size, &v, alpha, seed, ct.p.data(), 1),
+              "PublicKeyLv0.encryptBool");
+        return ct;
+    }
+};
+
+// proxy_reenc.zig:124-257: key_encryptions[(base*t*i)+(base*j)+k]; the c-th encryption uses seed0 + c.
+struct ProxyReencryptionKey {
+    std::vector<Torus> key_encryptions;
+    uint32_t basebit = 0, t = 0;
+    size_t base() const { return (size_t)1 << basebit; }
+
+    static ProxyReencryptionKey newSymmetricWithParams(const SecretKey &from, const SecretKey &to, double alpha,
+                                                       uint32_t basebit, uint32_t t, uint64_t seed0) {
+        ProxyReencryptionKey k = shaped(from.params, basebit, t);
+        check(tfhe_reenc_key_gen_symmetric(&from.params, from.key_lv0.data(), to.key_lv0.data(), alpha, basebit, t,
+                                           seed0, k.key_encryptions.data()),
+              "ProxyReencryptionKey.newSymmetric");
+        return k;
+    }
+    static ProxyReencryptionKey newAsymmetricWithParams(const SecretKey &from, const PublicKeyLv0 &to, double alpha,
+                                                        uint32_t basebit, uint32_t t, uint64_t seed0) {
+        ProxyReencryptionKey k = shaped(from.params, basebit, t);
+        check(tfhe_reenc_key_gen_asymmetric(&from.params, from.key_lv0.data(), to.encryptions.data(), to.size, alpha,
+                                            basebit, t, seed0, k.key_encryptions.data()),
+              "ProxyReencryptionKey.newAsymmetric");
+        return k;
+    }
+    // newSymmetric / newAsymmetric: KSK_ALPHA and the set's BASEBIT / IKS_T (:131-147, :199-212)
+    static ProxyReencryptionKey newSymmetric(const SecretKey &from, const SecretKey &to, uint64_t seed0) {
+        return newSymmetricWithParams(from, to, from.params.alpha_ksk, from.params.basebit, from.params.iks_t, seed0);
+    }
+    static ProxyReencryptionKey newAsymmetric(const SecretKey &from, const PublicKeyLv0 &to, uint64_t seed0) {
+        return newAsymmetricWithParams(from, to, from.params.alpha_ksk, from.params.basebit, from.params.iks_t, seed0);
+    }
+
+  private:
+    static ProxyReencryptionKey shaped(const tfhe_params &p, uint32_t basebit, uint32_t t) {
+        ProxyReencryptionKey k;
+        k.basebit = basebit;
+        k.t = t;
+        k.key_encryptions.assign(((size_t)p.n * t << basebit) * (p.n + 1), 0u);
+        return k;
+    }
 };
 
 // key.zig:61-118.  The cloud key lives in HBM inside one GPU context.
@@ -149,6 +227,43 @@ class CloudKey {
     }
     tfhe_params p_{};
     std::unique_ptr<tfhe_gpu_ctx, Del> ctx_;
+};
+
+// reencryptTLWELv0 (proxy_reenc.zig:267-306) on the GPU: the key is uploaded once to HBM; a
+// context of its own (no cloud key needed).
+class HipReencryptor {
+  public:
+    HipReencryptor(const tfhe_params &p, const ProxyReencryptionKey &k, int device = 0) : p_(p) {
+        tfhe_gpu_ctx *c = nullptr;
+        check(tfhe_gpu_create(&p, device, &c), "tfhe_gpu_create");
+        ctx_.reset(c);
+        tfhe_gpu_reenc_key *h = nullptr;
+        check(tfhe_gpu_reenc_key_load(c, k.key_encryptions.data(), k.key_encryptions.size(), k.basebit, k.t, &h),
+              "reenc_key_load", c);
+        key_.reset(h);
+    }
+    std::vector<TLWELv0> reencryptBatch(const std::vector<TLWELv0> &in) const {
+        const size_t w = p_.n + 1;
+        std::vector<Torus> x(in.size() * w), y(in.size() * w);
+        for (size_t k = 0; k < in.size(); k++) std::copy(in[k].p.begin(), in[k].p.end(), x.begin() + k * w);
+        check(tfhe_gpu_reencrypt_batch(ctx_.get(), key_.get(), x.data(), y.data(), in.size()), "reencrypt",
+              ctx_.get());
+        std::vector<TLWELv0> r(in.size(), TLWELv0(p_.n));
+        for (size_t k = 0; k < in.size(); k++) std::copy(y.begin() + k * w, y.begin() + (k + 1) * w, r[k].p.begin());
+        return r;
+    }
+    TLWELv0 reencryptTLWELv0(const TLWELv0 &ct) const { return reencryptBatch({ct})[0]; }
+
+  private:
+    struct DelCtx {
+        void operator()(tfhe_gpu_ctx *c) const { tfhe_gpu_destroy(c); }
+    };
+    struct DelKey {
+        void operator()(tfhe_gpu_reenc_key *k) const { tfhe_gpu_reenc_key_destroy(k); }
+    };
+    tfhe_params p_{};
+    std::unique_ptr<tfhe_gpu_ctx, DelCtx> ctx_;
+    std::unique_ptr<tfhe_gpu_reenc_key, DelKey> key_;  // declared after ctx_: destroyed first
 };
 
 // bootstrap.zig:30-47 strategy, vanilla.zig:38-75 semantics

@@ -206,6 +206,43 @@ uint32_t tlwe_phase(uint32_t n, const uint32_t *ct, const uint32_t *key) {
     return ct[n] - inner;
 }
 
+// PublicKeyLv0.encryptF64 (proxy_reenc.zig:83-113): plaintext on b, each
+// encryption of zero kept with probability 1/2 and added or subtracted with
+// probability 1/2 (two booleans, the second only when kept), then fresh noise.
+void pk_encrypt(uint32_t n, const uint32_t *pk, size_t pk_size, double plaintext, double alpha, uint64_t seed,
+                uint32_t *out) {
+    host::Rng r(seed);
+    std::fill(out, out + n + 1, 0u);
+    out[n] = host::f64_to_torus(plaintext);
+    for (size_t e = 0; e < pk_size; e++) {
+        if (!r.boolean()) continue;
+        const uint32_t *enc = pk + e * (n + 1);
+        if (r.boolean())
+            for (uint32_t x = 0; x <= n; x++) out[x] += enc[x];
+        else
+            for (uint32_t x = 0; x <= n; x++) out[x] -= enc[x];
+    }
+    host::NormalDist nd(0.0, alpha);
+    out[n] += host::gaussian_torus(0u, nd, r);
+}
+
+// ProxyReencryptionKey.new{Symmetric,Asymmetric}WithParams (proxy_reenc.zig:
+// 150-256): entry (i, j, k != 0) encrypts k * key_from[i] / 2^((j+1)*basebit)
+// under the target; the c-th encryption in (i, j, k) order uses seed0 + c.
+template <class Enc>
+void reenc_key_gen(uint32_t n, const uint32_t *key_from, uint32_t basebit, uint32_t t, uint64_t seed0,
+                   uint32_t *out, Enc enc) {
+    const uint32_t base = 1u << basebit;
+    std::fill(out, out + (size_t)n * t * base * (n + 1), 0u);
+    uint64_t c = 0;
+    for (uint32_t i = 0; i < n; i++)
+        for (uint32_t j = 0; j < t; j++)
+            for (uint32_t k = 1; k < base; k++) {
+                const double p = ((double)k * (double)key_from[i]) / (double)(1u << ((j + 1) * basebit));
+                enc(p, seed0 + c++, out + ((size_t)base * t * i + (size_t)base * j + k) * (n + 1));
+            }
+}
+
 }  // namespace
 
 extern "C" {
@@ -362,11 +399,7 @@ int tfhe_gpu_keygen(tfhe_gpu_ctx *c, uint64_t secret_seed, uint64_t cloud_seed, 
     const tfhe_params &p = c->P;
     const uint32_t N = p.N, n = p.n, L = p.L, T = p.iks_t, base = 1u << p.basebit;
     HIPCHK(c, hipSetDevice(c->device));
-    {  // SecretKey.new (key.zig:41-57)
-        host::Rng r(secret_seed);
-        for (uint32_t i = 0; i < n; i++) key_lv0[i] = r.boolean() ? 1u : 0u;
-        for (uint32_t i = 0; i < N; i++) key_lv1[i] = r.boolean() ? 1u : 0u;
-    }
+    tfhe_secret_key_new(&p, secret_seed, key_lv0, key_lv1);
     host::Rng master(cloud_seed);
     // genKeySwitchingKey (key.zig:148-172): k = 0 rows are zeroed
     std::vector<uint32_t> ksk(ksk_words(p), 0u);
@@ -519,6 +552,113 @@ int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint
                                (uint32_t *)c->s_out.p, B, RUN_BOOTSTRAP);
     if (!rc) rc = d2h_sync(c, out, c->s_out.p, B * w * 4);
     return rc;
+}
+
+// ---- Proxy re-encryption ------------------------------------
+}  // extern "C"
+
+struct tfhe_gpu_reenc_key {
+    int device = 0;
+    uint32_t basebit = 0, t = 0;
+    uint32_t *d_key = nullptr;  // padded rows like the KSK (K.ks_stride words) + zero tail
+};
+
+extern "C" {
+
+int tfhe_gpu_reenc_key_load(tfhe_gpu_ctx *c, const uint32_t *key_encryptions, size_t len, uint32_t basebit,
+                            uint32_t t, tfhe_gpu_reenc_key **out) {
+    if (!c || !key_encryptions || !out) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t n = c->P.n, rows = n * t * ((size_t)1 << basebit);
+    if (basebit < 1 || basebit > 8 || t < 1 || basebit * t >= 31 || !reencrypt_supported((int)t, (int)basebit))
+        return fail(c, TFHE_ERR_INVALID, "unsupported re-encryption base/levels");
+    if (len != rows * (n + 1)) return fail(c, TFHE_ERR_INVALID, "len != n*t*2^basebit*(n+1)");
+    HIPCHK(c, hipSetDevice(c->device));
+    auto *k = new tfhe_gpu_reenc_key;
+    k->device = c->device;
+    k->basebit = basebit;
+    k->t = t;
+    const size_t stride = c->K.ks_stride, bytes = (rows * stride + KS_TAIL_WORDS) * sizeof(uint32_t);
+    hipError_t e = hipMalloc((void **)&k->d_key, bytes);
+    if (e != hipSuccess) {
+        delete k;
+        return fail(c, TFHE_ERR_OOM, "hipMalloc(reencryption key)");
+    }
+    e = hipMemsetAsync(k->d_key, 0, bytes, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(k->d_key, stride * 4, key_encryptions, (n + 1) * 4, (n + 1) * 4, rows,
+                             hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_key_zero_k0(c->K, k->d_key, (int)n, (int)t, (int)basebit, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(k->d_key);
+        delete k;
+        return hip_fail(c, e, "upload reencryption key");
+    }
+    *out = k;
+    return TFHE_OK;
+}
+
+void tfhe_gpu_reenc_key_destroy(tfhe_gpu_reenc_key *k) {
+    if (!k) return;
+    (void)hipSetDevice(k->device);
+    (void)hipFree(k->d_key);
+    delete k;
+}
+
+int tfhe_gpu_reencrypt_batch(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const uint32_t *in, uint32_t *out,
+                             size_t B) {
+    if (!c || !k || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (k->device != c->device) return fail(c, TFHE_ERR_INVALID, "key belongs to another device");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = h2d(c, c->s_a, in, B * w * 4);
+    if (!rc) rc = ensure(c, c->s_out, B * w * 4);
+    if (rc) return rc;
+    HIPCHK(c, launch_reencrypt(c->K, (int)k->t, (int)k->basebit, (const uint32_t *)c->s_a.p, k->d_key,
+                               (uint32_t *)c->s_out.p, B, c->stream));
+    return d2h_sync(c, out, c->s_out.p, B * w * 4);
+}
+
+int tfhe_secret_key_new(const tfhe_params *p, uint64_t seed, uint32_t *key_lv0, uint32_t *key_lv1) {
+    if (!p || !key_lv0 || !key_lv1) return TFHE_ERR_INVALID;
+    host::Rng r(seed);  // SecretKey.new (key.zig:41-57)
+    for (uint32_t i = 0; i < p->n; i++) key_lv0[i] = r.boolean() ? 1u : 0u;
+    for (uint32_t i = 0; i < p->N; i++) key_lv1[i] = r.boolean() ? 1u : 0u;
+    return TFHE_OK;
+}
+
+int tfhe_public_key_gen(const tfhe_params *p, const uint32_t *key, size_t size, double alpha, uint64_t seed0,
+                        uint32_t *pk) {
+    if (!p || !key || (size && !pk)) return TFHE_ERR_INVALID;
+    for (size_t e = 0; e < size; e++) tlwe_encrypt(p->n, 0.0, alpha, key, seed0 + e, pk + e * (p->n + 1));
+    return TFHE_OK;
+}
+
+int tfhe_public_key_encrypt_bool_batch(const tfhe_params *p, const uint32_t *pk, size_t pk_size, const uint8_t *bits,
+                                       double alpha, uint64_t seed0, uint32_t *out, size_t B) {
+    if (!p || (pk_size && !pk) || (B && (!bits || !out))) return TFHE_ERR_INVALID;
+    for (size_t i = 0; i < B; i++)
+        pk_encrypt(p->n, pk, pk_size, bits[i] ? 0.125 : -0.125, alpha, seed0 + i, out + i * (p->n + 1));
+    return TFHE_OK;
+}
+
+int tfhe_reenc_key_gen_symmetric(const tfhe_params *p, const uint32_t *key_from, const uint32_t *key_to, double alpha,
+                                 uint32_t basebit, uint32_t t, uint64_t seed0, uint32_t *out) {
+    if (!p || !key_from || !key_to || !out || basebit < 1 || basebit > 8 || t < 1) return TFHE_ERR_INVALID;
+    reenc_key_gen(p->n, key_from, basebit, t, seed0, out, [&](double v, uint64_t seed, uint32_t *o) {
+        tlwe_encrypt(p->n, v, alpha, key_to, seed, o);
+    });
+    return TFHE_OK;
+}
+
+int tfhe_reenc_key_gen_asymmetric(const tfhe_params *p, const uint32_t *key_from, const uint32_t *pk, size_t pk_size,
+                                  double alpha, uint32_t basebit, uint32_t t, uint64_t seed0, uint32_t *out) {
+    if (!p || !key_from || !out || (pk_size && !pk) || basebit < 1 || basebit > 8 || t < 1) return TFHE_ERR_INVALID;
+    reenc_key_gen(p->n, key_from, basebit, t, seed0, out, [&](double v, uint64_t seed, uint32_t *o) {
+        pk_encrypt(p->n, pk, pk_size, v, alpha, seed, o);
+    });
+    return TFHE_OK;
 }
 
 // ---- Circuit evaluation with a level scheduler -------------

@@ -61,6 +61,13 @@ hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32
                              uint32_t *out, size_t B, hipStream_t s);
 // zero the k = 0 rows (never read by the reference; the kernels subtract them unconditionally)
 hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s);
+// same for a key-switch-shaped key over n_in input coefficients (proxy re-encryption key)
+hipError_t launch_key_zero_k0(const KParams &P, uint32_t *key, int n_in, int t, int basebit, hipStream_t s);
+// reencryptTLWELv0 (proxy_reenc.zig:267-306): key-switch-shaped key of n*t*2^basebit
+// rows in the padded device layout; in/out B TLWELv0
+hipError_t launch_reencrypt(const KParams &P, int t, int basebit, const uint32_t *in, const uint32_t *key,
+                            uint32_t *out, size_t B, hipStream_t s);
+bool reencrypt_supported(int t, int basebit);
 // key-switch kernel form: 0 = lanes (default), 1 = select/gather (development knob TFHE_KS_KERNEL)
 hipError_t launch_fft_forward(const DevTables &T, const uint32_t *in, double *out, size_t B,
                               hipStream_t s);

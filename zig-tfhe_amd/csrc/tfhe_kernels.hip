@@ -1258,9 +1258,13 @@ constexpr int KL_CHUNK = 32;  // output words per block (8 pieces of 16 B)
 constexpr int KL_WAVES = 4;
 
 template <int T, int BASEBIT>
+// n_in / in_stride: input dimension and words per input ciphertext — N and
+// N+1 for the identity key switch (TLWELv1 in), n and n+1 for the proxy
+// re-encryption of proxy_reenc.zig:267-306 (TLWELv0 in, same algorithm).
 __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint32_t *__restrict__ lv1,
                                                           const uint32_t *__restrict__ ksk,
-                                                          uint32_t *__restrict__ out, size_t B) {
+                                                          uint32_t *__restrict__ out, size_t B, int n_in,
+                                                          int in_stride) {
     constexpr int BASE = 1 << BASEBIT;
     constexpr int PIECES = KL_CHUNK / 4;
     constexpr int SLOTS = T * PIECES * BASE;    // 16-B slots per coefficient i
@@ -1279,7 +1283,8 @@ __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint3
     const int w0 = blockIdx.x * KL_CHUNK;
     const size_t rs = (size_t)P.ks_stride;
     const size_t step_i = (size_t)BASE * T * rs;  // words between consecutive i
-    const int ilo = w * (1024 / KL_WAVES), ihi = ilo + 1024 / KL_WAVES;
+    const int per = (n_in + KL_WAVES - 1) / KL_WAVES;
+    const int ilo = min(n_in, w * per), ihi = min(n_in, ilo + per);
     // this lane's DMA sources relative to row (i, 0, 0): slot s = c*64 + lane
     uint32_t src_off[NDMA];
 #pragma unroll
@@ -1295,7 +1300,7 @@ __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint3
     // their completion is counted by hand (vmcnt(0) at the top of step i, when
     // only buffer i's fill is in flight).
     const uint32_t ring_lds = (uint32_t)(size_t)(lds_void_t *)ring;
-    const uint32_t *a_src = lv1 + g * 1025;
+    const uint32_t *a_src = lv1 + g * (size_t)in_stride;
     auto issue = [&](int i, int which) {
         const uint32_t *r = ksk + (size_t)i * step_i;
 #pragma unroll
@@ -1320,7 +1325,7 @@ __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint3
     uint32_t acc[KL_CHUNK];
 #pragma unroll
     for (int x = 0; x < KL_CHUNK; x++) acc[x] = 0u;
-    issue(ilo, 0);
+    if (ilo < ihi) issue(ilo, 0);
     for (int i = ilo; i < ihi; i++) {
         const int cur = (i - ilo) & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // buffer i landed
@@ -1358,7 +1363,7 @@ __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint3
 #pragma unroll
         for (int v = 0; v < KL_WAVES; v++) r += red[(v * KL_CHUNK + x) * 64 + lane];
         const int word = w0 + x;
-        if (valid && word < n1) out[g * n1 + word] = (word == P.n ? a_src[1024] : 0u) + r;  // r = -(sum of rows)
+        if (valid && word < n1) out[g * n1 + word] = (word == P.n ? a_src[n_in] : 0u) + r;  // r = -(sum of rows)
     }
 }
 
@@ -1592,27 +1597,45 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     return hipGetLastError();
 }
 
+// lane-form key switch over an input of n_in coefficients (+ b); false if
+// (t, basebit) has no instantiation
+static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_t *in, int n_in, int in_stride,
+                            const uint32_t *key, uint32_t *out, size_t B, hipStream_t s) {
+    dim3 grid((unsigned)((P.ks_stride + KL_CHUNK - 1) / KL_CHUNK), (unsigned)((B + 63) / 64)), block(64 * KL_WAVES);
+#define KS_LANES(T_, BB_)                                                                                 \
+    hipLaunchKernelGGL((k_key_switch_lanes<T_, BB_>), grid, block, 0, s, P, in, key, out, B, n_in, in_stride)
+    if (basebit == 2 && t_ == 9) KS_LANES(9, 2);
+    else if (basebit == 2 && t_ == 8) KS_LANES(8, 2);
+    else if (basebit == 2 && t_ == 7) KS_LANES(7, 2);
+    else if (basebit == 3 && t_ == 4) KS_LANES(4, 3);
+    else if (basebit == 4 && t_ == 3) KS_LANES(3, 4);
+    else if (basebit == 4 && t_ == 4) KS_LANES(4, 4);
+    else if (basebit == 5 && t_ == 3) KS_LANES(3, 5);
+    else if (basebit == 5 && t_ == 2) KS_LANES(2, 5);
+    else return false;
+#undef KS_LANES
+    return true;
+}
+
+hipError_t launch_reencrypt(const KParams &P, int t_, int basebit, const uint32_t *in, const uint32_t *key,
+                            uint32_t *out, size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (!launch_ks_lanes(P, t_, basebit, in, P.n, P.n + 1, key, out, B, s)) return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+bool reencrypt_supported(int t_, int basebit) {
+    return (basebit == 2 && t_ >= 7 && t_ <= 9) || (basebit == 3 && t_ == 4) || (basebit == 4 && (t_ == 3 || t_ == 4)) ||
+           (basebit == 5 && (t_ == 2 || t_ == 3));
+}
+
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk, uint32_t *out,
                              size_t B, hipStream_t s) {
     if (B == 0) return hipSuccess;
     // kernel form: lanes (default) or the select/gather forms (TFHE_KS_KERNEL=sel, A/B and tests)
     const char *form = getenv("TFHE_KS_KERNEL");
-    if (!(form && form[0] == 's')) {
-        dim3 grid((unsigned)((P.ks_stride + KL_CHUNK - 1) / KL_CHUNK), (unsigned)((B + 63) / 64)), block(64 * KL_WAVES);
-#define KS_LANES(T_, BB_) hipLaunchKernelGGL((k_key_switch_lanes<T_, BB_>), grid, block, 0, s, P, lv1, ksk, out, B)
-        bool launched = true;
-        if (P.basebit == 2 && P.iks_t == 9) KS_LANES(9, 2);
-        else if (P.basebit == 2 && P.iks_t == 8) KS_LANES(8, 2);
-        else if (P.basebit == 2 && P.iks_t == 7) KS_LANES(7, 2);
-        else if (P.basebit == 3 && P.iks_t == 4) KS_LANES(4, 3);
-        else if (P.basebit == 4 && P.iks_t == 3) KS_LANES(3, 4);
-        else if (P.basebit == 4 && P.iks_t == 4) KS_LANES(4, 4);
-        else if (P.basebit == 5 && P.iks_t == 3) KS_LANES(3, 5);
-        else if (P.basebit == 5 && P.iks_t == 2) KS_LANES(2, 5);
-        else launched = false;  // other shapes: the general forms below
-#undef KS_LANES
-        if (launched) return hipGetLastError();
-    }
+    if (!(form && form[0] == 's') && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s))
+        return hipGetLastError();
     // items per block: development knob TFHE_KS_G in {8, 16, 32} (default 8)
     static const int G = [] {
         const char *e = getenv("TFHE_KS_G");
@@ -1650,8 +1673,12 @@ hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32
 }
 
 hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s) {
-    const int rs = P.ks_stride, base = 1 << P.basebit;
-    const size_t groups = (size_t)1024 * P.iks_t;
+    return launch_key_zero_k0(P, ksk, 1024, P.iks_t, P.basebit, s);
+}
+
+hipError_t launch_key_zero_k0(const KParams &P, uint32_t *ksk, int n_in, int t_, int basebit, hipStream_t s) {
+    const int rs = P.ks_stride, base = 1 << basebit;
+    const size_t groups = (size_t)n_in * t_;
     const size_t total = groups * rs;
     hipLaunchKernelGGL(k_ksk_zero_k0, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ksk, rs, base,
                        groups);

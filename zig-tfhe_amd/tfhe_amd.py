@@ -100,6 +100,17 @@ _SIGS = {
     "tfhe_decrypt_lwe_message_batch": (C.c_int, [C.POINTER(TfheParams), u32p, u32p, C.c_uint32, u32p,
                                                  C.c_size_t]),
     "tfhe_lut_generate": (C.c_int, [C.POINTER(TfheParams), C.c_uint32, u32p, u32p]),
+    "tfhe_secret_key_new": (C.c_int, [C.POINTER(TfheParams), C.c_uint64, u32p, u32p]),
+    "tfhe_gpu_reenc_key_load": (C.c_int, [vp, u32p, C.c_size_t, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
+    "tfhe_gpu_reenc_key_destroy": (None, [vp]),
+    "tfhe_gpu_reencrypt_batch": (C.c_int, [vp, vp, u32p, u32p, C.c_size_t]),
+    "tfhe_public_key_gen": (C.c_int, [C.POINTER(TfheParams), u32p, C.c_size_t, C.c_double, C.c_uint64, u32p]),
+    "tfhe_public_key_encrypt_bool_batch": (C.c_int, [C.POINTER(TfheParams), u32p, C.c_size_t, u8p, C.c_double,
+                                                     C.c_uint64, u32p, C.c_size_t]),
+    "tfhe_reenc_key_gen_symmetric": (C.c_int, [C.POINTER(TfheParams), u32p, u32p, C.c_double, C.c_uint32,
+                                               C.c_uint32, C.c_uint64, u32p]),
+    "tfhe_reenc_key_gen_asymmetric": (C.c_int, [C.POINTER(TfheParams), u32p, u32p, C.c_size_t, C.c_double,
+                                                C.c_uint32, C.c_uint32, C.c_uint64, u32p]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
@@ -383,6 +394,108 @@ class SecretKey:
                                                 out.ctypes.data_as(u32p), cts.shape[0])
         if rc:
             raise TfheError(f"decrypt_lwe_message: {rc}")
+        return out
+
+
+def secret_key_new(params: TfheParams, seed: int) -> SecretKey:
+    """key.SecretKey.new (key.zig:41-57) with DefaultPrng(seed) in place of getUniqueSeed()."""
+    lib = load_library()
+    k0, k1 = np.zeros(params.n, np.uint32), np.zeros(params.N, np.uint32)
+    rc = lib.tfhe_secret_key_new(C.byref(params), seed, k0.ctypes.data_as(u32p), k1.ctypes.data_as(u32p))
+    if rc:
+        raise TfheError(f"secret_key_new: {rc}")
+    return SecretKey(params, k0, k1)
+
+
+class PublicKeyLv0:
+    """proxy_reenc.PublicKeyLv0 (proxy_reenc.zig:35-121): `size` encryptions of zero under key_lv0.
+    Encryption e uses DefaultPrng(seed0 + e); size defaults to 2n (:44-54)."""
+
+    def __init__(self, sk: SecretKey, seed0: int, size: int | None = None, alpha: float | None = None):
+        p = self.params = sk.params
+        size = 2 * p.n if size is None else size
+        alpha = p.alpha_lv0 if alpha is None else alpha
+        self.encryptions = np.zeros((size, p.n + 1), np.uint32)
+        rc = load_library().tfhe_public_key_gen(C.byref(p), _u32(sk.key_lv0)[1], size, alpha, seed0,
+                                                self.encryptions.ctypes.data_as(u32p))
+        if rc:
+            raise TfheError(f"public_key_gen: {rc}")
+
+    def encrypt_bool(self, bits, seed0: int = 1, alpha: float | None = None):
+        """encryptBool (:116-120); item i uses DefaultPrng(seed0 + i)."""
+        p = self.params
+        alpha = p.alpha_lv0 if alpha is None else alpha
+        bits = np.ascontiguousarray(np.atleast_1d(bits), dtype=np.uint8)
+        out = np.zeros((bits.size, p.n + 1), np.uint32)
+        rc = load_library().tfhe_public_key_encrypt_bool_batch(
+            C.byref(p), self.encryptions.ctypes.data_as(u32p), self.encryptions.shape[0],
+            bits.ctypes.data_as(u8p), alpha, seed0, out.ctypes.data_as(u32p), bits.size)
+        if rc:
+            raise TfheError(f"public_key_encrypt_bool: {rc}")
+        return out
+
+
+class ProxyReencryptionKey:
+    """proxy_reenc.ProxyReencryptionKey (proxy_reenc.zig:124-257): key_encryptions[(base*t*i)+(base*j)+k]
+    = Enc_to(k * key_from[i] / 2^((j+1)*basebit)), k = 0 entries zero. Defaults: KSK_ALPHA and the
+    parameter set's BASEBIT / IKS_T (:131-147). The c-th encryption uses DefaultPrng(seed0 + c)."""
+
+    def __init__(self, key_encryptions: np.ndarray, basebit: int, t: int):
+        self.key_encryptions, self.basebit, self.t = key_encryptions, basebit, t
+        self.base = 1 << basebit
+
+    @classmethod
+    def _gen(cls, params, fn, extra, key_from, alpha, basebit, t, seed0):
+        alpha = params.alpha_ksk if alpha is None else alpha
+        basebit = params.basebit if basebit is None else basebit
+        t = params.iks_t if t is None else t
+        out = np.zeros(((1 << basebit) * t * params.n, params.n + 1), np.uint32)
+        rc = fn(C.byref(params), _u32(key_from)[1], *extra, alpha, basebit, t, seed0, out.ctypes.data_as(u32p))
+        if rc:
+            raise TfheError(f"reenc_key_gen: {rc}")
+        return cls(out, basebit, t)
+
+    @classmethod
+    def new_symmetric(cls, key_from: SecretKey, key_to: SecretKey, seed0: int, alpha=None, basebit=None, t=None):
+        """newSymmetricWithParams (:214-256)."""
+        return cls._gen(key_from.params, load_library().tfhe_reenc_key_gen_symmetric, [_u32(key_to.key_lv0)[1]],
+                        key_from.key_lv0, alpha, basebit, t, seed0)
+
+    @classmethod
+    def new_asymmetric(cls, key_from: SecretKey, pk_to: PublicKeyLv0, seed0: int, alpha=None, basebit=None,
+                       t=None):
+        """newAsymmetricWithParams (:150-196)."""
+        pk = pk_to.encryptions
+        return cls._gen(key_from.params, load_library().tfhe_reenc_key_gen_asymmetric,
+                        [pk.ctypes.data_as(u32p), pk.shape[0]], key_from.key_lv0, alpha, basebit, t, seed0)
+
+
+class HipReencryptor:
+    """reencryptTLWELv0 (proxy_reenc.zig:267-306) for a batch of TLWELv0, on the GPU: the re-encryption
+    key lives in HBM (padded rows, like the KSK) and each ciphertext is one lane of the key-switch kernel."""
+
+    def __init__(self, ctx: Context, key: ProxyReencryptionKey):
+        self.ctx, self.h = ctx, vp()
+        ke, kp = _u32(key.key_encryptions)
+        ctx.check(ctx.lib.tfhe_gpu_reenc_key_load(ctx.h, kp, ke.size, key.basebit, key.t, C.byref(self.h)),
+                  "reenc_key_load")
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.tfhe_gpu_reenc_key_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reencrypt(self, cts):
+        x, xp = _u32(np.atleast_2d(cts))
+        out = np.zeros_like(x)
+        self.ctx.check(self.ctx.lib.tfhe_gpu_reencrypt_batch(self.ctx.h, self.h, xp, out.ctypes.data_as(u32p),
+                                                             x.shape[0]), "reencrypt")
         return out
 
 
