@@ -287,6 +287,11 @@ int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
         std::vector<C2> tw2(tre.size()), st2(fre.size());
         for (size_t i = 0; i < tre.size(); i++) tw2[i] = C2{tre[i], tim[i]};
         for (size_t i = 0; i < fre.size(); i++) st2[i] = C2{fre[i], fim[i]};
+        // passA's bf_m1 (tfhe_kernels.hip) relies on W4[1].im == W8[2].im == -1.0 exactly
+        if (st2[2].y != -1.0 || st2[5].y != -1.0) {
+            rc = fail(c, TFHE_ERR_INVALID, "twiddle table: W4[1] / W8[2] imaginary part is not exactly -1");
+            break;
+        }
         c->twa[0] = st2[2];
         c->twa[1] = st2[4];
         c->twa[2] = st2[5];

@@ -91,6 +91,20 @@ DEV void bf1(C2 &u, C2 &x) {
     x = b;
 }
 
+// Butterfly with a twiddle whose imaginary part is exactly -1.0 in the
+// forward table (W4[1] and W8[2] of the recurrence; checked on the host when
+// the tables are built, tfhe_gpu.cpp): x.y * -1.0 == -x.y exactly, so the
+// reference's products by w.y are sign flips folded into the adds.  Same
+// results as bf<INV>(u, x, (wx, -1.0)) bit for bit, two multiplies fewer.
+template <bool INV>
+DEV void bf_m1(C2 &u, C2 &x, double wx) {
+    const C2 v = INV ? c2(x.x * wx - x.y, x.y * wx + x.x) : c2(x.x * wx + x.y, x.y * wx - x.x);
+    C2 a = c2(u.x + v.x, u.y + v.y);
+    C2 b = c2(u.x - v.x, u.y - v.y);
+    u = a;
+    x = b;
+}
+
 DEV int br3(int q) { return ((q & 1) << 2) | (q & 2) | ((q >> 2) & 1); }
 DEV int br6(int t) { return (int)(__builtin_bitreverse32((uint32_t)t) >> 26); }
 
@@ -162,8 +176,8 @@ struct LdsTw {
 template <bool INV>
 DEV void passA(C2 *d, const C2 *a) {
     bf1(d[0], d[1]); bf1(d[2], d[3]); bf1(d[4], d[5]); bf1(d[6], d[7]);
-    bf1(d[0], d[2]); bf<INV>(d[1], d[3], a[0]); bf1(d[4], d[6]); bf<INV>(d[5], d[7], a[0]);
-    bf1(d[0], d[4]); bf<INV>(d[1], d[5], a[1]); bf<INV>(d[2], d[6], a[2]); bf<INV>(d[3], d[7], a[3]);
+    bf1(d[0], d[2]); bf_m1<INV>(d[1], d[3], a[0].x); bf1(d[4], d[6]); bf_m1<INV>(d[5], d[7], a[0].x);
+    bf1(d[0], d[4]); bf<INV>(d[1], d[5], a[1]); bf_m1<INV>(d[2], d[6], a[2].x); bf<INV>(d[3], d[7], a[3]);
 }
 // Pass B: stages 16, 32, 64 (position bits 3-5 in q; j = (t&7) + 8*(...)).
 // Pass C: stages 128, 256, 512 (position bits 6-8 in q; j = t + 64*(...)).
@@ -307,10 +321,19 @@ DEV C2 twist_in(double xr, double xi, C2 w) { return c2(xr * w.x - xi * w.y, xr 
 
 // Untwist + normalisation of fft1024 (fft.zig:412-429).  `f` is 2x the
 // reference's value (the ×0.5 input scaling is folded), hence 1/(2*512).
+// NORM = false: the 2^-10 is already in `f` because the device BK is stored
+// scaled by 2^-10 (k_bk_permute); a power-of-two factor commutes with every
+// rounded add and multiply of the MAC, the inverse FFT and the untwist (no
+// overflow or subnormal at these magnitudes), so the results are identical.
+template <bool NORM = true>
 DEV void untwist_out(C2 f, C2 w, double &tr, double &ti) {
     const double norm = 1.0 / 1024.0;
-    tr = (f.x * w.x + f.y * w.y) * norm;
-    ti = (f.y * w.x - f.x * w.y) * norm;
+    tr = f.x * w.x + f.y * w.y;
+    ti = f.y * w.x - f.x * w.y;
+    if (NORM) {
+        tr = tr * norm;
+        ti = ti * norm;
+    }
 }
 
 // @round (half away from zero) -> i64 -> @truncate i32 -> u32 == r mod 2^32,
@@ -469,8 +492,8 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
     for (int q = 0; q < 8; q++) {
         double ra, ia, rb, ib;
         const C2 w = tws[q * TS];
-        untwist_out(e[0][q], w, ra, ia);
-        untwist_out(e[1][q], w, rb, ib);
+        untwist_out<false>(e[0][q], w, ra, ia);
+        untwist_out<false>(e[1][q], w, rb, ib);
         accA[q] += to_torus<SMALL>(ra);
         accA[q + 8] += to_torus<SMALL>(ia);
         accB[q] += to_torus<SMALL>(rb);
@@ -940,7 +963,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             double re, im;
-            untwist_out(e[0][q], twist_t[64 * q], re, im);
+            untwist_out<false>(e[0][q], twist_t[64 * q], re, im);
             acc[q] += to_torus<SMALL>(re);
             acc[q + 8] += to_torus<SMALL>(im);
         }
@@ -1098,7 +1121,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 double re, im;
-                untwist_out(e[0][q], twist_t[64 * q], re, im);
+                untwist_out<false>(e[0][q], twist_t[64 * q], re, im);
                 pa[t + 64 * q] += to_torus<SMALL>(re);
                 pa[t + 64 * q + 512] += to_torus<SMALL>(im);
             }
@@ -1510,16 +1533,19 @@ __global__ void k_bk_permute(const double *__restrict__ ref, double2 *__restrict
     const size_t rb = row * 2048;
     double2 *da = dev + row * 1024 + (size_t)(2 * q) * 64 + t;
     double2 *db = da + 64;
+    // device copy scaled by 2^-10 (exact): the untwist's 1/1024 moves into
+    // the key (untwist_out<false>)
+    const double down = 1.0 / 1024.0, up = 1024.0;
     if (dir == 0) {
-        *da = make_double2(ref[rb + pos], ref[rb + 512 + pos]);
-        *db = make_double2(ref[rb + 1024 + pos], ref[rb + 1536 + pos]);
+        *da = make_double2(ref[rb + pos] * down, ref[rb + 512 + pos] * down);
+        *db = make_double2(ref[rb + 1024 + pos] * down, ref[rb + 1536 + pos] * down);
     } else {
         double *r = const_cast<double *>(ref);
         double2 a = *da, b = *db;
-        r[rb + pos] = a.x;
-        r[rb + 512 + pos] = a.y;
-        r[rb + 1024 + pos] = b.x;
-        r[rb + 1536 + pos] = b.y;
+        r[rb + pos] = a.x * up;
+        r[rb + 512 + pos] = a.y * up;
+        r[rb + 1024 + pos] = b.x * up;
+        r[rb + 1536 + pos] = b.y * up;
     }
 }
 
