@@ -36,7 +36,8 @@ enum {
     TFHE_ERR_INVALID = -1,     /* bad argument / unsupported parameter set      */
     TFHE_ERR_HIP = -2,         /* HIP runtime error (no device, launch failure) */
     TFHE_ERR_NO_KEY = -3,      /* bootstrap requested before a cloud key loaded */
-    TFHE_ERR_OOM = -4          /* device allocation failed                      */
+    TFHE_ERR_OOM = -4,         /* device allocation failed                      */
+    TFHE_ERR_IO = -5           /* key file cannot be opened, read or written    */
 };
 
 /* Gate op codes — gates.zig:48-121 (pre-combination constants SURVEY §8a A2). */
@@ -99,6 +100,31 @@ int tfhe_gpu_export_key_device(tfhe_gpu_ctx *ctx, void *bsk_dev, void *ksk_dev,
                                uint32_t *decomposition_offset, uint32_t *testvec /*2N host*/);
 int tfhe_gpu_import_key_device(tfhe_gpu_ctx *ctx, const void *bsk_dev, const void *ksk_dev,
                                uint32_t decomposition_offset, const uint32_t *testvec /*2N host*/);
+/* The loaded CloudKey back in the reference's host layout (the inverse of
+ * tfhe_gpu_load_cloud_key; bsk: n*2L*2*N doubles, ksk: N*t*2^basebit*(n+1)
+ * words, the never-read k = 0 slots as zeros).  NULL outputs are skipped. */
+int tfhe_gpu_export_cloud_key(tfhe_gpu_ctx *ctx, uint32_t *decomposition_offset, uint32_t *testvec_a,
+                              uint32_t *testvec_b, double *bsk, uint32_t *ksk);
+
+/* ---- Cloud-key files (SURVEY §5 checkpoint row, §8f N3) -----------------
+ * The reference has no key serialization: every process regenerates its
+ * CloudKey (key.zig:70-77, ~30 s on a CPU).  A key file is a 64-byte header
+ * {char magic[8] = "ZTFHECK1"; u32 version = 1, n, N, L, bgbit, basebit,
+ * iks_t, decomposition_offset; u64 bsk_len, ksk_len, checksum} followed by
+ * testvec a (N u32), testvec b (N u32), the BootstrappingKey (bsk_len f64)
+ * and the KeySwitchingKey (ksk_len u32), all little-endian in the layouts
+ * above.  checksum = FNV-1a-64 over the four sections in 8-byte words.
+ * Reading checks the magic, the parameter set against `params` and the
+ * checksum (TFHE_ERR_INVALID); TFHE_ERR_IO: cannot open, short read/write. */
+int tfhe_cloud_key_write(const char *path, const tfhe_params *params, uint32_t decomposition_offset,
+                         const uint32_t *testvec_a, const uint32_t *testvec_b, const double *bsk, size_t bsk_len,
+                         const uint32_t *ksk, size_t ksk_len);
+int tfhe_cloud_key_read(const char *path, const tfhe_params *params, uint32_t *decomposition_offset,
+                        uint32_t *testvec_a, uint32_t *testvec_b, double *bsk, size_t bsk_len, uint32_t *ksk,
+                        size_t ksk_len);
+/* Export + write, and read + load, for a context (host memory for one key). */
+int tfhe_gpu_save_cloud_key(tfhe_gpu_ctx *ctx, const char *path);
+int tfhe_gpu_load_cloud_key_file(tfhe_gpu_ctx *ctx, const char *path);
 
 /* ---- Bootstrap / gates (host buffers, synchronous) ---------------------- */
 /* VanillaBootstrap.bootstrap (vanilla.zig:38-52) over B TLWELv0. */

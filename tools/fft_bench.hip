@@ -41,15 +41,15 @@ DEV void fft512_x3(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     passBC<INV>(d[2], wc_);
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256, 1) void k_bench(DevTables TT, double *out, int iters) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[8192 + 8192 + 4 * 16384];
+template <int MODE, int W = 1>
+__global__ __launch_bounds__(256 * W, 1) void k_bench(DevTables TT, double *out, int iters) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[8192 + 8192 + 4 * W * 16384];
     C2 *s_tw = reinterpret_cast<C2 *>(smem);
     C2 *s_twist = reinterpret_cast<C2 *>(smem + 8192);
     const int tid = threadIdx.x, t = tid & 63, w = tid >> 6;
     C2 *xb = reinterpret_cast<C2 *>(smem + 16384 + w * 16384);
-    for (int x = tid; x < 511; x += 256) s_tw[x] = TT.tw[x];
-    for (int x = tid; x < 512; x += 256) s_twist[x] = TT.twist[x];
+    for (int x = tid; x < 511; x += 256 * W) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 256 * W) s_twist[x] = TT.twist[x];
     __syncthreads();
     LdsTw T;
     T.init(s_tw, TT);
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256, 1) void k_bench(DevTables TT, double *out, int
     }
     double s = 0;
     for (int q = 0; q < 8; q++) s += d[0][q].x + d[1][q].y + d[2][q].x;
-    out[blockIdx.x * 256 + tid] = s;
+    out[blockIdx.x * 256 * W + tid] = s;
 }
 
 int main() {
@@ -93,7 +93,19 @@ int main() {
         hipEventRecord(b); hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b);
         // cycles per FFT per wave at 2.4 GHz (each iteration = 2 FFTs per wave)
-        if (rep) printf("%-32s %8.3f ms  %7.0f cycles per FFT per wave\n", nm[m], ms, ms * 1e-3 * 2.4e9 / (iters * (m == 4 ? 3.0 : 2.0)));
+        if (rep) printf("%-32s %8.3f ms  %7.0f cycles per FFT per wave  %6.1f ns per FFT per SIMD\n", nm[m], ms,
+                        ms * 1e-3 * 2.4e9 / (iters * (m == 4 ? 3.0 : 2.0)), ms * 1e6 / (iters * (m == 4 ? 3.0 : 2.0)));
+    }
+    // two waves per SIMD (8 waves per CU, wave-private exchange buffers): SIMD throughput
+    for (int rep = 0; rep < 2; rep++)
+    for (int m = 0; m < 3; m++) {
+        hipEventRecord(a);
+        if (m == 0) hipLaunchKernelGGL((k_bench<0, 2>), dim3(blocks), dim3(512), 0, 0, T, out, iters);
+        if (m == 1) hipLaunchKernelGGL((k_bench<1, 2>), dim3(blocks), dim3(512), 0, 0, T, out, iters);
+        if (m == 2) hipLaunchKernelGGL((k_bench<2, 2>), dim3(blocks), dim3(512), 0, 0, T, out, iters);
+        hipEventRecord(b); hipEventSynchronize(b);
+        float ms; hipEventElapsedTime(&ms, a, b);
+        if (rep) printf("2 waves/SIMD: %-32s %8.3f ms  %6.1f ns per FFT per SIMD\n", nm[m], ms, ms * 1e6 / (iters * 2.0 * 2));
     }
     return 0;
 }

@@ -140,6 +140,15 @@ int main() {
         expect(ok >= 90, "proxy reencryption chain asymmetric", "accuracy");
         std::printf("ok   proxy reencryption (symmetric, asymmetric, chain: %d/100)\n", ok);
     }
+    {  // key file: CloudKey.save -> CloudKey.loadFile drives the same gate (no reference counterpart)
+        const std::string path = "/tmp/tfhe_cpp_mirror_ck128.key";
+        ck.save(path);
+        const CloudKey ck2 = CloudKey::loadFile(params::SECURITY_128_BIT(), path);
+        const TLWELv0 x = enc(true), y = enc(false);
+        expect(gates.nandGate(x, y, ck).p == gates.nandGate(x, y, ck2).p, "key file", "same NAND bits");
+        std::remove(path.c_str());
+        std::printf("ok   key file save / loadFile\n");
+    }
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
     return failures ? 1 : 0;
 }

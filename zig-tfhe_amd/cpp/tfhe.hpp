@@ -213,6 +213,16 @@ class CloudKey {
               "CloudKey.load", ck.ctx());
         return ck;
     }
+    // Key files (include/tfhe_gpu.h "Cloud-key files"): the reference has no
+    // serialization; a saved key reloads bit-exact on any device.
+    static CloudKey loadFile(const tfhe_params &p, const std::string &path, int device = 0) {
+        CloudKey ck(p, device);
+        check(tfhe_gpu_load_cloud_key_file(ck.ctx(), path.c_str()), "CloudKey.loadFile", ck.ctx());
+        return ck;
+    }
+    void save(const std::string &path) const {
+        check(tfhe_gpu_save_cloud_key(ctx(), path.c_str()), "CloudKey.save", ctx());
+    }
     tfhe_gpu_ctx *ctx() const { return ctx_.get(); }
     const tfhe_params &params() const { return p_; }
 

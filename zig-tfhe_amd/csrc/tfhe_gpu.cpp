@@ -395,6 +395,151 @@ int tfhe_gpu_import_key_device(tfhe_gpu_ctx *c, const void *bsk_dev, const void 
     return TFHE_OK;
 }
 
+// Device key -> reference host layout: BK un-permuted (and un-scaled) by
+// k_bk_permute's inverse, KSK rows un-padded.
+int tfhe_gpu_export_cloud_key(tfhe_gpu_ctx *c, uint32_t *offset, uint32_t *tv_a, uint32_t *tv_b, double *bsk,
+                              uint32_t *ksk) {
+    if (!c) return TFHE_ERR_INVALID;
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t N = c->P.N;
+    if (offset) *offset = c->offset;
+    if (tv_a) std::memcpy(tv_a, c->testvec.data(), N * sizeof(uint32_t));
+    if (tv_b) std::memcpy(tv_b, c->testvec.data() + N, N * sizeof(uint32_t));
+    if (bsk) {
+        const size_t rows = bk_rows(c->P), bytes = rows * 2 * N * sizeof(double);
+        int rc = ensure(c, c->s_tmp, bytes);
+        if (rc) return rc;
+        HIPCHK(c, launch_bk_unpermute(c->K, c->d_bk, (double *)c->s_tmp.p, rows, c->stream));
+        HIPCHK(c, hipMemcpyAsync(bsk, c->s_tmp.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (ksk) {
+        const size_t w = c->P.n + 1;
+        HIPCHK(c, hipMemcpy2DAsync(ksk, w * 4, c->d_ksk, (size_t)c->K.ks_stride * 4, w * 4, ksk_rows(c->P),
+                                   hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TFHE_OK;
+}
+
+}  // extern "C"
+
+// ---- Cloud-key files (include/tfhe_gpu.h) ---------------
+namespace {
+
+struct KeyFileHeader {
+    char magic[8];
+    uint32_t version, n, N, L, bgbit, basebit, iks_t, offset;
+    uint64_t bsk_len, ksk_len, checksum;
+};
+static_assert(sizeof(KeyFileHeader) == 64, "key file header is 64 bytes");
+constexpr char KEY_MAGIC[8] = {'Z', 'T', 'F', 'H', 'E', 'C', 'K', '1'};
+
+// FNV-1a-64 over 8-byte little-endian words; a section's last < 8 bytes one by one
+struct Fnv64 {
+    uint64_t h = 0xcbf29ce484222325ull;
+    void add(const void *p, size_t bytes) {
+        const unsigned char *b = static_cast<const unsigned char *>(p);
+        size_t k = 0;
+        for (; k + 8 <= bytes; k += 8) {
+            uint64_t w;
+            std::memcpy(&w, b + k, 8);
+            h = (h ^ w) * 0x100000001b3ull;
+        }
+        for (; k < bytes; k++) h = (h ^ b[k]) * 0x100000001b3ull;
+    }
+};
+
+uint64_t key_checksum(const tfhe_params *p, const uint32_t *tv_a, const uint32_t *tv_b, const double *bsk,
+                      size_t bsk_len, const uint32_t *ksk, size_t ksk_len) {
+    Fnv64 f;
+    f.add(tv_a, p->N * sizeof(uint32_t));
+    f.add(tv_b, p->N * sizeof(uint32_t));
+    f.add(bsk, bsk_len * sizeof(double));
+    f.add(ksk, ksk_len * sizeof(uint32_t));
+    return f.h;
+}
+
+bool key_shape_ok(const tfhe_params *p, size_t bsk_len, size_t ksk_len) {
+    std::string why;
+    return params_ok(p, why) && bsk_len == bk_rows(*p) * 2 * p->N && ksk_len == ksk_words(*p);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfhe_cloud_key_write(const char *path, const tfhe_params *p, uint32_t offset, const uint32_t *tv_a,
+                         const uint32_t *tv_b, const double *bsk, size_t bsk_len, const uint32_t *ksk,
+                         size_t ksk_len) {
+    if (!path || !tv_a || !tv_b || !bsk || !ksk || !key_shape_ok(p, bsk_len, ksk_len)) return TFHE_ERR_INVALID;
+    KeyFileHeader h{};
+    std::memcpy(h.magic, KEY_MAGIC, 8);
+    h.version = 1;
+    h.n = p->n, h.N = p->N, h.L = p->L, h.bgbit = p->bgbit, h.basebit = p->basebit, h.iks_t = p->iks_t;
+    h.offset = offset;
+    h.bsk_len = bsk_len;
+    h.ksk_len = ksk_len;
+    h.checksum = key_checksum(p, tv_a, tv_b, bsk, bsk_len, ksk, ksk_len);
+    FILE *fp = std::fopen(path, "wb");
+    if (!fp) return TFHE_ERR_IO;
+    bool ok = std::fwrite(&h, sizeof h, 1, fp) == 1 && std::fwrite(tv_a, 4, p->N, fp) == p->N &&
+              std::fwrite(tv_b, 4, p->N, fp) == p->N && std::fwrite(bsk, 8, bsk_len, fp) == bsk_len &&
+              std::fwrite(ksk, 4, ksk_len, fp) == ksk_len;
+    ok = std::fclose(fp) == 0 && ok;
+    return ok ? TFHE_OK : TFHE_ERR_IO;
+}
+
+int tfhe_cloud_key_read(const char *path, const tfhe_params *p, uint32_t *offset, uint32_t *tv_a, uint32_t *tv_b,
+                        double *bsk, size_t bsk_len, uint32_t *ksk, size_t ksk_len) {
+    if (!path || !offset || !tv_a || !tv_b || !bsk || !ksk || !key_shape_ok(p, bsk_len, ksk_len))
+        return TFHE_ERR_INVALID;
+    FILE *fp = std::fopen(path, "rb");
+    if (!fp) return TFHE_ERR_IO;
+    KeyFileHeader h{};
+    int rc = TFHE_OK;
+    if (std::fread(&h, sizeof h, 1, fp) != 1)
+        rc = TFHE_ERR_IO;
+    else if (std::memcmp(h.magic, KEY_MAGIC, 8) != 0 || h.version != 1)
+        rc = TFHE_ERR_INVALID;  // not a key file of this format
+    else if (h.n != p->n || h.N != p->N || h.L != p->L || h.bgbit != p->bgbit || h.basebit != p->basebit ||
+             h.iks_t != p->iks_t || h.bsk_len != bsk_len || h.ksk_len != ksk_len)
+        rc = TFHE_ERR_INVALID;  // another parameter set
+    else if (std::fread(tv_a, 4, p->N, fp) != p->N || std::fread(tv_b, 4, p->N, fp) != p->N ||
+             std::fread(bsk, 8, bsk_len, fp) != bsk_len || std::fread(ksk, 4, ksk_len, fp) != ksk_len)
+        rc = TFHE_ERR_IO;  // truncated
+    std::fclose(fp);
+    if (rc) return rc;
+    if (key_checksum(p, tv_a, tv_b, bsk, bsk_len, ksk, ksk_len) != h.checksum) return TFHE_ERR_INVALID;
+    *offset = h.offset;
+    return TFHE_OK;
+}
+
+int tfhe_gpu_save_cloud_key(tfhe_gpu_ctx *c, const char *path) {
+    if (!c || !path) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t N = c->P.N, bl = bk_rows(c->P) * 2 * N, kl = ksk_words(c->P);
+    std::vector<uint32_t> ta(N), tb(N), ksk(kl);
+    std::vector<double> bsk(bl);
+    uint32_t off = 0;
+    int rc = tfhe_gpu_export_cloud_key(c, &off, ta.data(), tb.data(), bsk.data(), ksk.data());
+    if (rc) return rc;
+    rc = tfhe_cloud_key_write(path, &c->P, off, ta.data(), tb.data(), bsk.data(), bl, ksk.data(), kl);
+    if (rc) return fail(c, rc, std::string("cannot write key file ") + path);
+    return TFHE_OK;
+}
+
+int tfhe_gpu_load_cloud_key_file(tfhe_gpu_ctx *c, const char *path) {
+    if (!c || !path) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t N = c->P.N, bl = bk_rows(c->P) * 2 * N, kl = ksk_words(c->P);
+    std::vector<uint32_t> ta(N), tb(N), ksk(kl);
+    std::vector<double> bsk(bl);
+    uint32_t off = 0;
+    int rc = tfhe_cloud_key_read(path, &c->P, &off, ta.data(), tb.data(), bsk.data(), bl, ksk.data(), kl);
+    if (rc == TFHE_ERR_IO) return fail(c, rc, std::string("cannot read key file ") + path);
+    if (rc) return fail(c, rc, std::string(path) + ": not a key file of this parameter set, or checksum mismatch");
+    return tfhe_gpu_load_cloud_key(c, off, ta.data(), tb.data(), bsk.data(), bl, ksk.data(), kl);
+}
+
 // SecretKey.new + CloudKey.new, seeded.  Host: every RNG draw in reference
 // order; device: the FFT-based poly_mul of each TRLWE encryption
 // (trlwe.zig:56-61) and the TRGSWLv1FFT forward transforms (trgsw.zig:81-91).

@@ -77,6 +77,13 @@ _SIGS = {
     "tfhe_gpu_key_blob_bytes": (C.c_int, [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     "tfhe_gpu_export_key_device": (C.c_int, [vp, vp, vp, u32p, u32p]),
     "tfhe_gpu_import_key_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p]),
+    "tfhe_gpu_export_cloud_key": (C.c_int, [vp, C.POINTER(C.c_uint32), u32p, u32p, f64p, u32p]),
+    "tfhe_cloud_key_write": (C.c_int, [C.c_char_p, C.POINTER(TfheParams), C.c_uint32, u32p, u32p, f64p, C.c_size_t,
+                                       u32p, C.c_size_t]),
+    "tfhe_cloud_key_read": (C.c_int, [C.c_char_p, C.POINTER(TfheParams), C.POINTER(C.c_uint32), u32p, u32p, f64p,
+                                      C.c_size_t, u32p, C.c_size_t]),
+    "tfhe_gpu_save_cloud_key": (C.c_int, [vp, C.c_char_p]),
+    "tfhe_gpu_load_cloud_key_file": (C.c_int, [vp, C.c_char_p]),
     "tfhe_gpu_bootstrap_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_bootstrap_without_key_switch_batch": (C.c_int, [vp, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_gate_batch": (C.c_int, [vp, u8p, u32p, u32p, u32p, C.c_size_t]),
@@ -208,6 +215,26 @@ class Context:
         self.check(self.lib.tfhe_gpu_keygen(self.h, secret_seed, cloud_seed, k0.ctypes.data_as(u32p),
                                             k1.ctypes.data_as(u32p), bkp, kp), "keygen")
         return SecretKey(p, k0, k1), (bk, ksk)
+
+    def export_cloud_key(self):
+        """The loaded CloudKey in the reference layout: (offset, testvec 2N, bk (n,2L,2,N) f64,
+        ksk (N*t*2^basebit, n+1) u32; k = 0 rows zero)."""
+        p = self.params
+        off = C.c_uint32()
+        tv = np.zeros(2 * p.N, np.uint32)
+        bk = np.zeros((p.n, 2 * p.L, 2, p.N), np.float64)
+        ksk = np.zeros((p.N * p.iks_t * (1 << p.basebit), p.n + 1), np.uint32)
+        self.check(self.lib.tfhe_gpu_export_cloud_key(self.h, C.byref(off), tv[:p.N].ctypes.data_as(u32p),
+                                                      tv[p.N:].ctypes.data_as(u32p), bk.ctypes.data_as(f64p),
+                                                      ksk.ctypes.data_as(u32p)), "export_cloud_key")
+        return off.value, tv, bk, ksk
+
+    def save_cloud_key(self, path: str):
+        """Key file (include/tfhe_gpu.h 'Cloud-key files'): the reference has no serialization."""
+        self.check(self.lib.tfhe_gpu_save_cloud_key(self.h, os.fsencode(path)), "save_cloud_key")
+
+    def load_cloud_key_file(self, path: str):
+        self.check(self.lib.tfhe_gpu_load_cloud_key_file(self.h, os.fsencode(path)), "load_cloud_key_file")
 
     def key_blob_bytes(self):
         a, b = C.c_size_t(), C.c_size_t()
@@ -508,6 +535,36 @@ def lut_generate(params: TfheParams, m: int, f) -> np.ndarray:
     if rc:
         raise TfheError(f"lut_generate: {rc}")
     return tv
+
+
+def cloud_key_write(path: str, params: TfheParams, offset: int, testvec, bk, ksk):
+    """Write a CloudKey (reference layout) as a key file; host only (tfhe_cloud_key_write)."""
+    lib = load_library()
+    tv, _ = _u32(testvec)
+    bk, bkp = _f64(bk)
+    ksk, kp = _u32(ksk)
+    N = params.N
+    rc = lib.tfhe_cloud_key_write(os.fsencode(path), C.byref(params), offset, tv[:N].ctypes.data_as(u32p),
+                                  tv[N:].ctypes.data_as(u32p), bkp, bk.size, kp, ksk.size)
+    if rc:
+        raise TfheError(f"cloud_key_write: status {rc}")
+
+
+def cloud_key_read(path: str, params: TfheParams):
+    """-> (offset, testvec 2N, bk (n,2L,2,N), ksk (N*t*2^basebit, n+1)); raises TfheError
+    (status -5: I/O, -1: not a key file of this parameter set or checksum mismatch)."""
+    lib = load_library()
+    p = params
+    off = C.c_uint32()
+    tv = np.zeros(2 * p.N, np.uint32)
+    bk = np.zeros((p.n, 2 * p.L, 2, p.N), np.float64)
+    ksk = np.zeros((p.N * p.iks_t * (1 << p.basebit), p.n + 1), np.uint32)
+    rc = lib.tfhe_cloud_key_read(os.fsencode(path), C.byref(p), C.byref(off), tv[:p.N].ctypes.data_as(u32p),
+                                 tv[p.N:].ctypes.data_as(u32p), bk.ctypes.data_as(f64p), bk.size,
+                                 ksk.ctypes.data_as(u32p), ksk.size)
+    if rc:
+        raise TfheError(f"cloud_key_read: status {rc}")
+    return off.value, tv, bk, ksk
 
 
 class HipBootstrap:
