@@ -41,15 +41,26 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int rep = 0; rep < 2; rep++) {
-        unsigned long long z[8] = {0};
+        unsigned long long z[64] = {0};
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
         CK(hipEventRecord(e0));
         CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0));
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-        unsigned long long c[8];
+        unsigned long long c[64];
         CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
+        const char *form = getenv("TFHE_BR_KERNEL");
+        if (form && form[0] == 'w') {  // latency form: per wave, per phase (ticks per step per gate)
+            const char *wn[7] = {"digits+fwd+publish", "barrier1", "mac+prefetch", "barrier2", "inverse+add", "barrier3", "tail"};
+            printf("rep %d: %.3f ms (%zu gates); s_memtime ticks per step, per wave:\n", rep, ms, B);
+            for (int k = 0; k < 6; k++) {
+                printf("  %-20s", wn[k]);
+                for (int w = 0; w < 8; w++) printf(" %8.1f", c[w * 8 + k] / (double)B / P.n);
+                printf("\n");
+            }
+            continue;
+        }
         const char *nm[8] = {"tmp", "fwd-fft(pairs)", "barrier1", "mac", "barrier2", "inverse+add", "tail", "dma-issue"};
         double tot = 0;
         for (int k = 0; k < 8; k++) tot += c[k];

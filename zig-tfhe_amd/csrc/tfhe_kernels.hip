@@ -54,7 +54,7 @@ struct PhaseProf {
 #endif
 };
 #ifdef TFHE_PHASE_PROF
-__device__ unsigned long long g_phase_cycles[8];
+__device__ unsigned long long g_phase_cycles[64];  // [wave][phase] for the wide form
 #endif
 
 DEV C2 c2(double x, double y) {
@@ -1061,7 +1061,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     __syncthreads();
 
     int at_next = s_at[0];  // a~ read one step ahead (its wait would drain every LDS op)
+    PhaseProf pp;  // development timing (TFHE_PHASE_PROF), per wave
+    pp.start();
     for (int i = 0; i < n; i++) {
+        pp.mark(0);
         const int at = __builtin_amdgcn_readfirstlane(at_next);
         at_next = s_at[i + 1 < n ? i + 1 : i];
         if (w < 2 * L) {
@@ -1090,7 +1093,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
 #pragma unroll
             for (int q = 0; q < 8; q++) s_slot[w][t + 64 * q] = d[0][q];  // publish (after this wave's exchanges)
         }
+        pp.mark(1);
         __syncthreads();  // every row's spectrum is in its slot
+        pp.mark(2);
         const int f = t + 64 * w;
         C2 fa = c2(0.0, 0.0), fb = c2(0.0, 0.0);  // fmaInFd1024 accumulates from 0.0
 #pragma unroll
@@ -1111,7 +1116,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
         // frequency f of slots 0/1 is read and rewritten by this lane only
         s_slot[0][f] = fa;
         s_slot[1][f] = fb;
+        pp.mark(3);
         __syncthreads();  // both product spectra complete
+        pp.mark(4);
         if (w < 2) {
             C2 e[1][8];
 #pragma unroll
@@ -1126,8 +1133,14 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
                 pa[t + 64 * q + 512] += to_torus<SMALL>(im);
             }
         }
+        pp.mark(5);
         __syncthreads();  // accumulator updated
     }
+    pp.mark(6);
+#ifdef TFHE_PHASE_PROF
+    if (t == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[w * 8 + k], (unsigned long long)pp.acc[k]);
+#endif
 
     if (w != 0) return;
     if (out_mode == BR_OUT_LV1) {
