@@ -526,6 +526,30 @@ class HipReencryptor:
         return out
 
 
+class bit_utils:
+    """bit_utils.zig (host-side plaintext plumbing of the examples): `convert` (:9-16) packs
+    bits LSB first into an unsigned integer; `AsBits(T).toBits` (:24-27, :42-50) unpacks the
+    width of T; `AsBits(T).encrypt` (:29-39) encrypts every bit (DefaultPrng(seed0 + i) per bit
+    in place of getUniqueSeed())."""
+
+    @staticmethod
+    def convert(bits, width: int | None = None) -> int:
+        bits = list(bits)
+        width = len(bits) if width is None else width
+        v = 0
+        for i, b in enumerate(bits[:width]):
+            v |= (1 if b else 0) << i
+        return v
+
+    @staticmethod
+    def to_bits(value: int, width: int) -> np.ndarray:
+        return np.array([(int(value) >> i) & 1 for i in range(width)], dtype=bool)
+
+    @staticmethod
+    def encrypt(value: int, width: int, sk: SecretKey, seed0: int = 1) -> np.ndarray:
+        return sk.encrypt_bool(bit_utils.to_bits(value, width).astype(np.uint8), seed0=seed0)
+
+
 def lut_generate(params: TfheParams, m: int, f) -> np.ndarray:
     """Generator.generateLookupTable (lut/generator.zig:85-135) for f: x -> f(x), x < m."""
     lib = load_library()
