@@ -1292,23 +1292,29 @@ __global__ void k_ksk_zero_k0(uint32_t *__restrict__ ksk, int rs, int base, size
 // touch distinct banks.
 constexpr int KL_CHUNK = 32;  // output words per block (8 pieces of 16 B)
 constexpr int KL_WAVES = 4;
+// Balanced variant for the 128-bit set at B = 1024: 44-word chunks (16 per
+// 704-word padded row) x 8 waves -> exactly 256 blocks, one per CU, instead of
+// 352 blocks of which 96 share a CU (launch_ks_lanes picks per batch).
+constexpr int KL_CHUNK_WIDE = 44;
+constexpr int KL_WAVES_WIDE = 8;
 
-template <int T, int BASEBIT>
+template <int T, int BASEBIT, int CHUNK = KL_CHUNK, int WAVES = KL_WAVES>
 // n_in / in_stride: input dimension and words per input ciphertext — N and
 // N+1 for the identity key switch (TLWELv1 in), n and n+1 for the proxy
 // re-encryption of proxy_reenc.zig:267-306 (TLWELv0 in, same algorithm).
-__global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint32_t *__restrict__ lv1,
+__global__ __launch_bounds__(64 * WAVES) void k_key_switch_lanes(KParams P, const uint32_t *__restrict__ lv1,
                                                           const uint32_t *__restrict__ ksk,
                                                           uint32_t *__restrict__ out, size_t B, int n_in,
                                                           int in_stride) {
     constexpr int BASE = 1 << BASEBIT;
-    constexpr int PIECES = KL_CHUNK / 4;
+    constexpr int PIECES = CHUNK / 4;
     constexpr int SLOTS = T * PIECES * BASE;    // 16-B slots per coefficient i
     constexpr int NDMA = (SLOTS + 63) / 64;     // LDS-DMA instructions per i
     constexpr int BUF = NDMA * 64 + 16;         // 16-B slots per buffer: KSK slots + 64 digits words
     constexpr int RING = 2 * BUF;               // double buffer
-    constexpr int RED = KL_WAVES * KL_CHUNK * 64;  // reduction words
-    constexpr int LDS_BYTES = (RING * 16 * KL_WAVES > RED * 4) ? RING * 16 * KL_WAVES : RED * 4;
+    constexpr int RED = WAVES * CHUNK * 64;     // reduction words
+    constexpr int LDS_BYTES = (RING * 16 * WAVES > RED * 4) ? RING * 16 * WAVES : RED * 4;
+    static_assert(LDS_BYTES <= 160 * 1024, "key-switch LDS");
     __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1316,10 +1322,10 @@ __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint3
     const size_t g_raw = (size_t)blockIdx.y * 64 + lane;
     const bool valid = g_raw < B;
     const size_t g = valid ? g_raw : B - 1;
-    const int w0 = blockIdx.x * KL_CHUNK;
+    const int w0 = blockIdx.x * CHUNK;
     const size_t rs = (size_t)P.ks_stride;
     const size_t step_i = (size_t)BASE * T * rs;  // words between consecutive i
-    const int per = (n_in + KL_WAVES - 1) / KL_WAVES;
+    const int per = (n_in + WAVES - 1) / WAVES;
     const int ilo = min(n_in, w * per), ihi = min(n_in, ilo + per);
     // this lane's DMA sources relative to row (i, 0, 0): slot s = c*64 + lane
     uint32_t src_off[NDMA];
@@ -1358,9 +1364,9 @@ __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint3
             : "memory");
     };
     const uint32_t prec = 1u << (32 - (1 + BASEBIT * T));
-    uint32_t acc[KL_CHUNK];
+    uint32_t acc[CHUNK];
 #pragma unroll
-    for (int x = 0; x < KL_CHUNK; x++) acc[x] = 0u;
+    for (int x = 0; x < CHUNK; x++) acc[x] = 0u;
     if (ilo < ihi) issue(ilo, 0);
     for (int i = ilo; i < ihi; i++) {
         const int cur = (i - ilo) & 1;
@@ -1388,16 +1394,13 @@ __global__ __launch_bounds__(256) void k_key_switch_lanes(KParams P, const uint3
     __syncthreads();  // every wave done with its ring: reuse LDS for the reduction
     uint32_t *red = reinterpret_cast<uint32_t *>(smem);
 #pragma unroll
-    for (int x = 0; x < KL_CHUNK; x++) red[(w * KL_CHUNK + x) * 64 + lane] = acc[x];
+    for (int x = 0; x < CHUNK; x++) red[(w * CHUNK + x) * 64 + lane] = acc[x];
     __syncthreads();
     const int n1 = P.n + 1;
-    constexpr int PER = KL_CHUNK / KL_WAVES;
-#pragma unroll
-    for (int y = 0; y < PER; y++) {
-        const int x = w * PER + y;
+    for (int x = w; x < CHUNK; x += WAVES) {  // wave w reduces words w, w + WAVES, ...
         uint32_t r = 0u;
 #pragma unroll
-        for (int v = 0; v < KL_WAVES; v++) r += red[(v * KL_CHUNK + x) * 64 + lane];
+        for (int v = 0; v < WAVES; v++) r += red[(v * CHUNK + x) * 64 + lane];
         const int word = w0 + x;
         if (valid && word < n1) out[g * n1 + word] = (word == P.n ? a_src[n_in] : 0u) + r;  // r = -(sum of rows)
     }
@@ -1640,7 +1643,26 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
 // (t, basebit) has no instantiation
 static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_t *in, int n_in, int in_stride,
                             const uint32_t *key, uint32_t *out, size_t B, hipStream_t s) {
-    dim3 grid((unsigned)((P.ks_stride + KL_CHUNK - 1) / KL_CHUNK), (unsigned)((B + 63) / 64)), block(64 * KL_WAVES);
+    const unsigned groups = (unsigned)((B + 63) / 64);
+    dim3 grid((unsigned)((P.ks_stride + KL_CHUNK - 1) / KL_CHUNK), groups), block(64 * KL_WAVES);
+    // basebit 2 (128/80-bit): the 44-word x 8-wave blocks when they spread the
+    // work more evenly over the 256 CUs (rounds of one block per CU x pieces per
+    // block); 1024 gates at 128-bit: 1 round x 11 pieces instead of 2 x 8
+    const unsigned wide_chunks = (unsigned)((P.ks_stride + KL_CHUNK_WIDE - 1) / KL_CHUNK_WIDE);
+    const size_t rounds = (grid.x * (size_t)groups + 255) / 256, rounds_w = (wide_chunks * (size_t)groups + 255) / 256;
+    const bool wide = basebit == 2 && !getenv("TFHE_KS_NARROW") && rounds_w * (KL_CHUNK_WIDE / 4) < rounds * (KL_CHUNK / 4);
+    if (wide) {
+        dim3 gw(wide_chunks, groups), bw(64 * KL_WAVES_WIDE);
+#define KS_WIDE(T_)                                                                                                     \
+    hipLaunchKernelGGL((k_key_switch_lanes<T_, 2, KL_CHUNK_WIDE, KL_WAVES_WIDE>), gw, bw, 0, s, P, in, key, out, B, \
+                       n_in, in_stride)
+        if (t_ == 9) KS_WIDE(9);
+        else if (t_ == 8) KS_WIDE(8);
+        else if (t_ == 7) KS_WIDE(7);
+        else return false;
+#undef KS_WIDE
+        return true;
+    }
 #define KS_LANES(T_, BB_)                                                                                 \
     hipLaunchKernelGGL((k_key_switch_lanes<T_, BB_>), grid, block, 0, s, P, in, key, out, B, n_in, in_stride)
     if (basebit == 2 && t_ == 9) KS_LANES(9, 2);
