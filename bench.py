@@ -60,6 +60,9 @@ def f64_ops_per_cmux(L: int) -> int:
 
 
 VALU_F64_PEAK = 256 * 4 * 16 * 2.4e9  # non-FMA f64 ops/s: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz (78.6 TF FMA spec / 2)
+# measured with tools/isa_rate.hip (profiles/r01_isa_rate.txt): independent v_add_f64 / v_mul_f64
+# at 4 waves per SIMD issue every 2.01 ns per SIMD -> 1024 SIMDs x 64 lanes / 2.01 ns
+VALU_F64_SUSTAINED = 1024 * 64 / 2.01e-9
 
 
 def cpu_baseline(p, sk, bk, ksk, A, B, gpu_out, seconds: float):
@@ -325,7 +328,9 @@ def main():
                          "kernel": f"k_blind_rotate<{p.L}> ({form} form)", "kernel_avg_ms": round(br_avg_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": alg},
             "valu_f64": {"achieved": round(f64_rate / 1e12, 2), "peak": round(VALU_F64_PEAK / 1e12, 1),
-                         "unit": "Tops/s (f64 add+mul, no FMA)", "frac": round(f64_rate / VALU_F64_PEAK, 4)},
+                         "unit": "Tops/s (f64 add+mul, no FMA)", "frac": round(f64_rate / VALU_F64_PEAK, 4),
+                         "peak_sustained": round(VALU_F64_SUSTAINED / 1e12, 1),
+                         "frac_sustained": round(f64_rate / VALU_F64_SUSTAINED, 4)},
             "key_switch_avg_ms": round(ks_avg_s * 1e3, 3),
             "decrypt_check": all_correct,
         }
