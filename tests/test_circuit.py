@@ -109,3 +109,38 @@ def test_circuit_rejects_bad_graphs(oracle):
                                   np.array([1, 0], np.uint32))  # no gates: outputs are inputs
     assert depth == 0 and np.array_equal(out, x[[1, 0]])
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_circuit_ragged_levels_tail_form(oracle, monkeypatch):
+    """Levels of 1,030 gates: a 1,024-gate whole-form round plus a 6-gate tail that
+    launch_blind_rotate hands to the latency form (inputs gathered by index in both).
+    Bit-identical to forcing the whole form for the full level, and level-1
+    samples (tail included) bit-exact vs the oracle."""
+    from conftest import get_keys
+    k = get_keys(oracle, "80")
+    ctx = tfhe_amd.Context("80", 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    sk = tfhe_amd.SecretKey(ctx.params, k.k0, k.k1)
+    g = np.random.default_rng(11)
+    c = Circuit()
+    ins = [c.input() for _ in range(40)]
+    pairs = g.integers(0, 40, (1030, 2))
+    lvl1 = [c.and_(ins[x], ins[y]) if i % 2 else c.xor(ins[x], ins[y]) for i, (x, y) in enumerate(pairs)]
+    lvl2 = [c.or_(lvl1[i], lvl1[(i * 7 + 3) % 1030]) for i in range(1030)]
+    c.output(*lvl1, *lvl2)
+    bits = g.integers(0, 2, 40)
+    inputs = sk.encrypt_bool(bits.astype(np.uint8), seed0=900)
+    got, depth = c.run(ctx, inputs)
+    assert depth == 2
+    l1 = np.array([(bits[x] & bits[y]) if i % 2 else (bits[x] ^ bits[y]) for i, (x, y) in enumerate(pairs)], bool)
+    l2 = np.array([l1[i] | l1[(i * 7 + 3) % 1030] for i in range(1030)], bool)
+    assert np.array_equal(sk.decrypt_bool(got), np.concatenate([l1, l2]))
+    monkeypatch.setenv("TFHE_BR_KERNEL", "whole")
+    forced, _ = c.run(ctx, inputs)
+    assert np.array_equal(got, forced)
+    for i in (0, 511, 1023, 1024, 1027, 1029):  # level-1 gates; 1024.. are the tail
+        op = tfhe_amd.AND if i % 2 else tfhe_amd.XOR
+        want = oracle.gate_batch(k.p, np.array([op], np.uint8), inputs[pairs[i][0]][None], inputs[pairs[i][1]][None], k.ck)
+        assert np.array_equal(got[i], want[0])
+    ctx.close()

@@ -1590,10 +1590,10 @@ hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint3
     return hipGetLastError();
 }
 
-hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
+static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
-                               hipStream_t s) {
+                               hipStream_t s, char forced) {
     if (B == 0) return hipSuccess;
     const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
     // |external product| <= 2L * N * Bg/2 * 2^31: the 8-op exact conversion
@@ -1602,10 +1602,9 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     // kernel form: wide (8 waves per item) for batches up to BR_WIDE_MAX_ITEMS,
     // else whole (1 wave per item); split (2 waves per item) on request.
     // Knob TFHE_BR_KERNEL=whole|split|wide forces a form (A/B runs and tests).
-    const char *form = getenv("TFHE_BR_KERNEL");
-    const bool split = form && form[0] == 's';
-    // latency form for batches below one gate per SIMD pair (TFHE_BR_KERNEL=wide forces it)
-    const bool wide = form ? form[0] == 'W' || (form[0] == 'w' && form[1] == 'i') : B <= BR_WIDE_MAX_ITEMS;
+    const bool split = forced == 's';
+    // latency form for batches below one gate per SIMD pair
+    const bool wide = forced ? forced == 'W' : B <= BR_WIDE_MAX_ITEMS;
     dim3 grid, block;
     if (wide) {
         grid = dim3((unsigned)B);
@@ -1637,6 +1636,45 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     }
 #undef BR_LAUNCH
     return hipGetLastError();
+}
+
+// Kernel form per batch.  TFHE_BR_KERNEL=whole|split|wide forces one form for
+// the whole batch (A/B runs and tests).  Otherwise: the latency form up to
+// BR_WIDE_MAX_ITEMS; above it the whole form, except that a ragged last round
+// of at most BR_TAIL_WIDE_MAX items (the whole form runs 4 items x #CUs per
+// round) goes to the latency form, which takes ~4.4 ms for it instead of a
+// full ~9.5 ms round (a circuit level of 10,256 gates: 99 vs 106 ms).
+constexpr size_t BR_TAIL_WIDE_MAX = 256;
+
+hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
+                               const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                               const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
+                               hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    const char *form = getenv("TFHE_BR_KERNEL");
+    if (form) {
+        const char f = form[0] == 's' ? 's' : (form[0] == 'W' || (form[0] == 'w' && form[1] == 'i')) ? 'W' : 'w';
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f);
+    }
+    if (B <= BR_WIDE_MAX_ITEMS) return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 0);
+    static int cus = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return v > 0 ? v : 256;
+    }();
+    const size_t round = (size_t)BR_WAVES * cus, tail = B % round;
+    if (tail == 0 || tail > BR_TAIL_WIDE_MAX || B < round)
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'w');
+    const size_t main = B - tail;
+    hipError_t e = launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, main, s, 'w');
+    if (e != hipSuccess) return e;
+    // the tail: items main..B-1 (their ops / idx entries / inputs / outputs)
+    const size_t in_words = (size_t)P.n + 1;
+    const size_t out_words = out_mode == BR_OUT_LV1 ? (size_t)P.N + 1 : out_mode == BR_OUT_TRLWE ? 2 * (size_t)P.N : in_words;
+    return launch_blind_rotate_form(P, T, ops ? ops + main : nullptr, idx ? in_a : in_a + main * in_words,
+                                    idx ? in_b : (in_b ? in_b + main * in_words : nullptr), idx ? idx + 2 * main : nullptr,
+                                    testvec, bkd, out + main * out_words, out_mode, tail, s, 'W');
 }
 
 // lane-form key switch over an input of n_in coefficients (+ b); false if
