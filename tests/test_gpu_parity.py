@@ -282,3 +282,21 @@ def test_device_resident_api_with_torch(oracle):
     finally:
         c.set_stream(None)
     assert np.array_equal(t_o.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.parametrize("gw", ["1", "2", "4"])
+def test_lut_uint4_key_switch_item_groups(oracle, monkeypatch, gw):
+    """UINT4 key switch with 1, 2 or 4 item groups per block (TFHE_KS_GW; 4 is the
+    default above 64 items): 300 LUT bootstraps, outputs identical across forms,
+    samples past the first group bit-exact vs the oracle."""
+    c, k = ctx_for(oracle, "uint4")
+    tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (3 * x + 5) % 16)
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    msgs = rng(23).integers(0, 16, 300).astype(np.uint32)
+    cts = sk.encrypt_lwe_message(msgs, 16, seed0=4242)
+    monkeypatch.setenv("TFHE_KS_GW", gw)
+    out = c.bootstrap_lut_batch(cts, tv)
+    assert np.array_equal(sk.decrypt_lwe_message(out, 16), (3 * msgs + 5) % 16)
+    for i in (0, 63, 64, 200, 299):
+        want = oracle.gate_batch(k.p, np.array([255], np.uint8), cts[i][None], cts[i][None], k.ck, testvec=tv)[0]
+        assert np.array_equal(out[i], want)

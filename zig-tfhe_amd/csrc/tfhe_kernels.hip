@@ -1298,10 +1298,14 @@ constexpr int KL_WAVES = 4;
 constexpr int KL_CHUNK_WIDE = 44;
 constexpr int KL_WAVES_WIDE = 8;
 
-template <int T, int BASEBIT, int CHUNK = KL_CHUNK, int WAVES = KL_WAVES>
+template <int T, int BASEBIT, int CHUNK = KL_CHUNK, int WAVES = KL_WAVES, int GW = 1>
 // n_in / in_stride: input dimension and words per input ciphertext — N and
 // N+1 for the identity key switch (TLWELv1 in), n and n+1 for the proxy
 // re-encryption of proxy_reenc.zig:267-306 (TLWELv0 in, same algorithm).
+// GW: waves that take different 64-item groups (64*GW items per block) and
+// walk the same coefficients in the same order, so their DMAs of one KSK
+// chunk meet in L2; the other WAVES/GW split the coefficient range.  GW > 1
+// cuts KSK reads from HBM when the key does not stay cached (UINT4: 323 MB).
 __global__ __launch_bounds__(64 * WAVES) void k_key_switch_lanes(KParams P, const uint32_t *__restrict__ lv1,
                                                           const uint32_t *__restrict__ ksk,
                                                           uint32_t *__restrict__ out, size_t B, int n_in,
@@ -1318,15 +1322,18 @@ __global__ __launch_bounds__(64 * WAVES) void k_key_switch_lanes(KParams P, cons
     __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int IW = WAVES / GW;  // waves splitting the coefficient range
+    static_assert(WAVES % GW == 0, "GW divides WAVES");
+    const int gw = w % GW, iw = w / GW;
     uint4 *ring = reinterpret_cast<uint4 *>(smem) + w * RING;
-    const size_t g_raw = (size_t)blockIdx.y * 64 + lane;
+    const size_t g_raw = (size_t)blockIdx.y * (64 * GW) + gw * 64 + lane;
     const bool valid = g_raw < B;
     const size_t g = valid ? g_raw : B - 1;
     const int w0 = blockIdx.x * CHUNK;
     const size_t rs = (size_t)P.ks_stride;
     const size_t step_i = (size_t)BASE * T * rs;  // words between consecutive i
-    const int per = (n_in + WAVES - 1) / WAVES;
-    const int ilo = min(n_in, w * per), ihi = min(n_in, ilo + per);
+    const int per = (n_in + IW - 1) / IW;
+    const int ilo = min(n_in, iw * per), ihi = min(n_in, ilo + per);
     // this lane's DMA sources relative to row (i, 0, 0): slot s = c*64 + lane
     uint32_t src_off[NDMA];
 #pragma unroll
@@ -1397,10 +1404,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_key_switch_lanes(KParams P, cons
     for (int x = 0; x < CHUNK; x++) red[(w * CHUNK + x) * 64 + lane] = acc[x];
     __syncthreads();
     const int n1 = P.n + 1;
-    for (int x = w; x < CHUNK; x += WAVES) {  // wave w reduces words w, w + WAVES, ...
+    for (int x = iw; x < CHUNK; x += IW) {  // wave (gw, iw) reduces words iw, iw + IW, ... of group gw
         uint32_t r = 0u;
 #pragma unroll
-        for (int v = 0; v < WAVES; v++) r += red[(v * CHUNK + x) * 64 + lane];
+        for (int v = 0; v < IW; v++) r += red[((v * GW + gw) * CHUNK + x) * 64 + lane];
         const int word = w0 + x;
         if (valid && word < n1) out[g * n1 + word] = (word == P.n ? a_src[n_in] : 0u) + r;  // r = -(sum of rows)
     }
@@ -1699,6 +1706,25 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
         else if (t_ == 7) KS_WIDE(7);
         else return false;
 #undef KS_WIDE
+        return true;
+    }
+    // UINT4 (basebit 5): the 323 MB KSK streams from HBM once per item group, so
+    // 4 groups per block share each chunk through L2 (TFHE_KS_GW=1 forces one)
+    const char *gw_e = getenv("TFHE_KS_GW");
+    const int gw_env = gw_e ? atoi(gw_e) : 0;
+    const int gw = gw_env ? gw_env : (basebit >= 5 ? 4 : 1);
+    if (gw == 4 && basebit == 5 && B > 64) {
+        dim3 g4(grid.x, (unsigned)((B + 255) / 256)), b4(256);
+        if (t_ == 3) hipLaunchKernelGGL((k_key_switch_lanes<3, 5, KL_CHUNK, 4, 4>), g4, b4, 0, s, P, in, key, out, B, n_in, in_stride);
+        else if (t_ == 2) hipLaunchKernelGGL((k_key_switch_lanes<2, 5, KL_CHUNK, 4, 4>), g4, b4, 0, s, P, in, key, out, B, n_in, in_stride);
+        else return false;
+        return true;
+    }
+    if (gw == 2 && basebit == 5 && B > 64) {
+        dim3 g2(grid.x, (unsigned)((B + 127) / 128)), b2(256);
+        if (t_ == 3) hipLaunchKernelGGL((k_key_switch_lanes<3, 5, KL_CHUNK, 4, 2>), g2, b2, 0, s, P, in, key, out, B, n_in, in_stride);
+        else if (t_ == 2) hipLaunchKernelGGL((k_key_switch_lanes<2, 5, KL_CHUNK, 4, 2>), g2, b2, 0, s, P, in, key, out, B, n_in, in_stride);
+        else return false;
         return true;
     }
 #define KS_LANES(T_, BB_)                                                                                 \
