@@ -106,7 +106,34 @@ def oracle_vectors():
              gate_ops=ops, gate_a=A, gate_b=B, gate_out=out, gate_params="80", sk_seed=42, ck_seed=43)
 
 
+
+
+def gates128_vectors():
+    """The headline configuration's bits: the 128-bit cloud key from
+    seeds (sk 42, ck 43), one gate of each op plus NANDs, 700-step blind rotations and the
+    key switch, stored as inputs + outputs + sha256 of the outputs (the 172 MB key is
+    regenerated from the seeds)."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle, params
+    o = Oracle()
+    p = params("128")
+    k0, k1 = o.secret_key(p, 42)
+    ck = o.cloud_key(p, 43, k0, k1)
+    g = np.random.default_rng(128)
+    ops = np.concatenate([np.arange(10), np.zeros(6)]).astype(np.uint8)
+    bits_a = g.integers(0, 2, ops.size)
+    bits_b = g.integers(0, 2, ops.size)
+    A = np.array([o.tlwe_encrypt_bool(p.n, a, p.alpha_lv0, k0, 17000 + i) for i, a in enumerate(bits_a)])
+    B = np.array([o.tlwe_encrypt_bool(p.n, b, p.alpha_lv0, k0, 18000 + i) for i, b in enumerate(bits_b)])
+    out = o.gate_batch(p, ops, A, B, ck, threads=8)
+    digest = hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest()
+    np.savez(os.path.join(HERE, "gates128.npz"), ops=ops, a=A, b=B, bits_a=bits_a, bits_b=bits_b, out=out,
+             out_sha256=digest, params="128", sk_seed=42, ck_seed=43)
+    print("gates128 sha256", digest)
+
+
 if __name__ == "__main__":
-    twiddles()
-    polymul_bigint()
-    oracle_vectors()
+    what = sys.argv[1:] or ["twiddles", "polymul_bigint", "oracle_vectors", "gates128_vectors"]
+    for name in what:
+        globals()[name]()

@@ -300,3 +300,17 @@ def test_lut_uint4_key_switch_item_groups(oracle, monkeypatch, gw):
     for i in (0, 63, 64, 200, 299):
         want = oracle.gate_batch(k.p, np.array([255], np.uint8), cts[i][None], cts[i][None], k.ck, testvec=tv)[0]
         assert np.array_equal(out[i], want)
+
+
+def test_gates128_golden_fixture():
+    """BASELINE config 2's parameter set against committed bits, no oracle on the box:
+    tfhe_gpu_keygen(42, 43) (bit-equal to the oracle's keygen, test_keygen_matches_oracle)
+    then one gate of each op plus NANDs vs tests/golden/gates128.npz."""
+    import hashlib
+    g = np.load(os.path.join(GOLDEN, "gates128.npz"))
+    c = tfhe_amd.Context("128", 0)
+    c.keygen(42, 43)
+    out = c.gate_batch(g["ops"], g["a"], g["b"])
+    assert hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest() == str(g["out_sha256"])
+    assert np.array_equal(out, g["out"])
+    c.close()

@@ -313,3 +313,22 @@ def test_add_two_numbers_16bit(oracle, keys80):  # examples/add_two_numbers.zig:
         carry = gate(1, a_and_b, x_and_c)
     val = sum(int(oracle.tlwe_decrypt_bool(p.n, b, k.k0)) << i for i, b in enumerate(bits))
     assert val == 706
+
+
+def test_gates128_golden(oracle):
+    """The headline parameter set pinned by a committed fixture (tests/golden/gates128.npz):
+    keys from seeds 42/43, one gate of each op plus NANDs, 700-step blind rotations + key
+    switch; the oracle reproduces the committed outputs and their sha256."""
+    import hashlib
+    g = np.load(os.path.join(GOLDEN, "gates128.npz"))
+    k = get_keys(oracle, "128")
+    out = oracle.gate_batch(k.p, g["ops"], g["a"], g["b"], k.ck, threads=8)
+    assert hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest() == str(g["out_sha256"])
+    assert np.array_equal(out, g["out"])
+    # and they decrypt to the gates' truth tables (xnorGate: reference semantics, decrypts as XOR)
+    truth = {0: lambda a, b: 1 - (a & b), 1: lambda a, b: a | b, 2: lambda a, b: a & b, 3: lambda a, b: a ^ b,
+             4: lambda a, b: a ^ b, 5: lambda a, b: 1 - (a | b), 6: lambda a, b: (1 - a) & b,
+             7: lambda a, b: a & (1 - b), 8: lambda a, b: (1 - a) | b, 9: lambda a, b: a | (1 - b)}
+    dec = [oracle.tlwe_decrypt_bool(k.p.n, c, k.k0) for c in out]
+    want = [bool(truth[int(o)](int(a), int(b))) for o, a, b in zip(g["ops"], g["bits_a"], g["bits_b"])]
+    assert dec == want
