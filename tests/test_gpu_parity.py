@@ -284,7 +284,7 @@ def test_device_resident_api_with_torch(oracle):
     assert np.array_equal(t_o.cpu().numpy().view(np.uint32), want)
 
 
-@pytest.mark.parametrize("gw", ["1", "2", "4"])
+@pytest.mark.parametrize("gw", ["1", "2", "4", "8"])
 def test_lut_uint4_key_switch_item_groups(oracle, monkeypatch, gw):
     """UINT4 key switch with 1, 2 or 4 item groups per block (TFHE_KS_GW; 4 is the
     default above 64 items): 300 LUT bootstraps, outputs identical across forms,

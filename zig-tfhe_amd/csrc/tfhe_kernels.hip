@@ -1713,6 +1713,11 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
     const char *gw_e = getenv("TFHE_KS_GW");
     const int gw_env = gw_e ? atoi(gw_e) : 0;
     const int gw = gw_env ? gw_env : (basebit >= 5 ? 4 : 1);
+    if (gw == 8 && basebit == 5 && t_ == 3 && B > 64) {  // 16-word chunks: 8 rings fit the LDS
+        dim3 g8((unsigned)((P.ks_stride + 15) / 16), (unsigned)((B + 511) / 512)), b8(512);
+        hipLaunchKernelGGL((k_key_switch_lanes<3, 5, 16, 8, 8>), g8, b8, 0, s, P, in, key, out, B, n_in, in_stride);
+        return true;
+    }
     if (gw == 4 && basebit == 5 && B > 64) {
         dim3 g4(grid.x, (unsigned)((B + 255) / 256)), b4(256);
         if (t_ == 3) hipLaunchKernelGGL((k_key_switch_lanes<3, 5, KL_CHUNK, 4, 4>), g4, b4, 0, s, P, in, key, out, B, n_in, in_stride);
