@@ -1018,7 +1018,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
     __shared__ __attribute__((aligned(16))) C2 s_tw[512];
     __shared__ __attribute__((aligned(16))) C2 s_twist[512];
-    __shared__ __attribute__((aligned(16))) C2 s_slot[2 * L][512];
+    // row r's product spectra (a, b) in s_prod[0/1][r]; s_prod[0][r] is also row
+    // wave r's FFT exchange buffer, and slots 0/1 of s_prod[0] receive the sums
+    __shared__ __attribute__((aligned(16))) C2 s_prod[2][2 * L][512];
     __shared__ __attribute__((aligned(16))) uint32_t s_acc[2048];
     __shared__ uint16_t s_at[1024];
     __shared__ int s_bt;
@@ -1043,12 +1045,14 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
             else s_bt = 2048 - (int)tl;
         }
     }
-    // this wave's BK words of step 0: rows r, parts a|b, frequency t + 64w
-    double2 kb[2 * L][2];
+    // row wave r's BK words of step 0: row r, parts a|b, every frequency t + 64q
+    double2 kr[8][2];
+    if (w < 2 * L) {
 #pragma unroll
-    for (int r = 0; r < 2 * L; r++)
+        for (int q = 0; q < 8; q++)
 #pragma unroll
-        for (int h = 0; h < 2; h++) kb[r][h] = bkd[((size_t)r * 8 + w) * 128 + h * 64 + t];
+            for (int h = 0; h < 2; h++) kr[q][h] = bkd[((size_t)w * 8 + q) * 128 + h * 64 + t];
+    }
     __syncthreads();
     const int bt = __builtin_amdgcn_readfirstlane(s_bt);
     if (w < 2) {
@@ -1089,41 +1093,45 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
                 const uint32_t x1 = (n1 ? 0u - rot[m + 8] : rot[m + 8]) - own[m + 8] + P.offset;
                 d[0][q] = twist_in(digit_f64(x0, level, P.bgbit), digit_f64(x1, level, P.bgbit), twist_t[64 * m]);
             }
-            fft512<1, false>(d, s_slot[w], T, t);
+            fft512<1, false>(d, s_prod[0][w], T, t);
+            // this row's terms of fmaInFd1024 for both outputs, every frequency
+            // (after this wave's exchanges in s_prod[0][w])
 #pragma unroll
-            for (int q = 0; q < 8; q++) s_slot[w][t + 64 * q] = d[0][q];  // publish (after this wave's exchanges)
+            for (int q = 0; q < 8; q++) {
+                s_prod[0][w][t + 64 * q] = cmul_bk(d[0][q], kr[q][0]);
+                s_prod[1][w][t + 64 * q] = cmul_bk(d[0][q], kr[q][1]);
+            }
+            if (i + 1 < n) {  // next step's BK row, landing under the sum, inverse and forward phases
+                const double2 *nb = bkd + (size_t)(i + 1) * trgsw;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++) kr[q][h] = nb[((size_t)w * 8 + q) * 128 + h * 64 + t];
+            }
         }
         pp.mark(1);
-        __syncthreads();  // every row's spectrum is in its slot
+        __syncthreads();  // every row's terms are in place
         pp.mark(2);
+        // sum in the reference's row order 0..2L-1 (fmaInFd1024 starts from 0.0: 0.0 + x == x)
         const int f = t + 64 * w;
-        C2 fa = c2(0.0, 0.0), fb = c2(0.0, 0.0);  // fmaInFd1024 accumulates from 0.0
+        C2 fa = s_prod[0][0][f], fb = s_prod[1][0][f];
 #pragma unroll
-        for (int r = 0; r < 2 * L; r++) {
-            const C2 x = s_slot[r][f];
-            const C2 ta = cmul_bk(x, kb[r][0]);
-            const C2 tb = cmul_bk(x, kb[r][1]);
+        for (int r = 1; r < 2 * L; r++) {
+            const C2 ta = s_prod[0][r][f], tb = s_prod[1][r][f];
             fa = c2(fa.x + ta.x, fa.y + ta.y);
             fb = c2(fb.x + tb.x, fb.y + tb.y);
         }
-        if (i + 1 < n) {  // next step's BK words, landing under the inverse and forward phases
-            const double2 *nb = bkd + (size_t)(i + 1) * trgsw;
-#pragma unroll
-            for (int r = 0; r < 2 * L; r++)
-#pragma unroll
-                for (int h = 0; h < 2; h++) kb[r][h] = nb[((size_t)r * 8 + w) * 128 + h * 64 + t];
-        }
-        // frequency f of slots 0/1 is read and rewritten by this lane only
-        s_slot[0][f] = fa;
-        s_slot[1][f] = fb;
+        // frequency f of slots 0/1 is read above and rewritten here by this lane only
+        s_prod[0][0][f] = fa;
+        s_prod[0][1][f] = fb;
         pp.mark(3);
         __syncthreads();  // both product spectra complete
         pp.mark(4);
         if (w < 2) {
             C2 e[1][8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) e[0][q] = s_slot[w][t + 64 * br3(q)];
-            fft512<1, true>(e, s_slot[w], T, t);
+            for (int q = 0; q < 8; q++) e[0][q] = s_prod[0][w][t + 64 * br3(q)];
+            fft512<1, true>(e, s_prod[0][w], T, t);
             uint32_t *pa = s_acc + w * 1024;
 #pragma unroll
             for (int q = 0; q < 8; q++) {
