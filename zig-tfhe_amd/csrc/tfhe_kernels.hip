@@ -1657,9 +1657,10 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
 // the whole batch (A/B runs and tests).  Otherwise: the latency form up to
 // BR_WIDE_MAX_ITEMS; above it the whole form, except that a ragged last round
 // of at most BR_TAIL_WIDE_MAX items (the whole form runs 4 items x #CUs per
-// round) goes to the latency form, which takes ~4.4 ms for it instead of a
-// full ~9.5 ms round (a circuit level of 10,256 gates: 99 vs 106 ms).
-constexpr size_t BR_TAIL_WIDE_MAX = 256;
+// round) goes to the latency form, which takes ~4.2 ms for up to 256 items and
+// ~8.1 ms for up to 512 instead of a full ~9.5 ms round (a circuit level of
+// 10,256 gates: 99 vs 106 ms).
+constexpr size_t BR_TAIL_WIDE_MAX = BR_WIDE_MAX_ITEMS;
 
 hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
