@@ -152,8 +152,11 @@ int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, const ui
  * inputs (TLWELv0 each); gate g drives wire n_inputs+g from wires in_a[g],
  * in_b[g] (both < n_inputs+g; in_b ignored for NOT/COPY).  ops: TFHE_GATE_*
  * (bootstrapped) or TFHE_GATE_NOT (free).  Each dependency level is one
- * batched bootstrap launch; every wire stays in HBM.  outputs receives the
- * n_outputs wires out_wires[]; *levels (may be NULL) the bootstrap depth. */
+ * batched bootstrap launch; every wire stays in HBM.  Gates with slack may
+ * run one level later than their earliest level when that avoids a ragged
+ * partial round (depth unchanged; env TFHE_CIRCUIT_PACK=0 disables it).
+ * outputs receives the n_outputs wires out_wires[]; *levels (may be NULL)
+ * the bootstrap depth. */
 int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
                           const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
                           const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels);

@@ -144,3 +144,49 @@ def test_circuit_ragged_levels_tail_form(oracle, monkeypatch):
         want = oracle.gate_batch(k.p, np.array([op], np.uint8), inputs[pairs[i][0]][None], inputs[pairs[i][1]][None], k.ck)
         assert np.array_equal(got[i], want[0])
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_circuit_round_packing(oracle, monkeypatch):
+    """Round packing: level 1 has 1,064 gates, 40 of which only drive outputs.
+    The scheduler moves those 40 to level 2 (one 1,024-gate round + a 140-gate
+    level) instead of running a 40-gate tail after the round.  Outputs are
+    bit-identical to the unpacked schedule (TFHE_CIRCUIT_PACK=0), decrypt to the
+    truth table, sample bit-exact vs the oracle, and the packed run is faster."""
+    import time
+    from conftest import get_keys
+    k = get_keys(oracle, "80")
+    ctx = tfhe_amd.Context("80", 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    sk = tfhe_amd.SecretKey(ctx.params, k.k0, k.k1)
+    g = np.random.default_rng(12)
+    c = Circuit()
+    ins = [c.input() for _ in range(40)]
+    pairs = g.integers(0, 40, (1064, 2))
+    lvl1 = [c.and_(ins[x], ins[y]) if i % 2 else c.xor(ins[x], ins[y]) for i, (x, y) in enumerate(pairs)]
+    lvl2 = [c.or_(lvl1[i], lvl1[i + 1]) for i in range(0, 200, 2)]  # uses gates 0..199 only
+    c.output(*lvl1, *lvl2)
+    bits = g.integers(0, 2, 40)
+    inputs = sk.encrypt_bool(bits.astype(np.uint8), seed0=901)
+
+    def timed():
+        c.run(ctx, inputs)
+        t0 = time.perf_counter()
+        out, depth = c.run(ctx, inputs)
+        return out, depth, time.perf_counter() - t0
+
+    got, depth, t_pack = timed()
+    assert depth == 2
+    l1 = np.array([(bits[x] & bits[y]) if i % 2 else (bits[x] ^ bits[y]) for i, (x, y) in enumerate(pairs)], bool)
+    l2 = np.array([l1[i] | l1[i + 1] for i in range(0, 200, 2)], bool)
+    assert np.array_equal(sk.decrypt_bool(got), np.concatenate([l1, l2]))
+    monkeypatch.setenv("TFHE_CIRCUIT_PACK", "0")
+    plain, _, t_plain = timed()
+    assert np.array_equal(got, plain)
+    for i in (0, 1023, 1024, 1063):  # 1024.. are the moved gates
+        op = tfhe_amd.AND if i % 2 else tfhe_amd.XOR
+        want = oracle.gate_batch(k.p, np.array([op], np.uint8), inputs[pairs[i][0]][None], inputs[pairs[i][1]][None], k.ck)
+        assert np.array_equal(got[i], want[0])
+    print(f"packed {t_pack * 1e3:.1f} ms, unpacked {t_plain * 1e3:.1f} ms")
+    assert t_pack < 0.9 * t_plain
+    ctx.close()

@@ -812,6 +812,74 @@ int tfhe_reenc_key_gen_asymmetric(const tfhe_params *p, const uint32_t *key_from
 }
 
 // ---- Circuit evaluation with a level scheduler -------------
+// Round packing.  A bootstrapped gate whose consumers all sit at least two
+// levels later, and that feeds no NOT, can run one level later without
+// changing the depth.  Levels are visited in ascending order; each moves to
+// the next level the number of such gates that minimises the modelled
+// blind-rotation time of the two levels (blind_rotate_cost: whole rounds of
+// 4 x #CUs gates, a ragged tail in the latency form).  Example: a level of
+// 10,256 gates hands 16 of them to the next level instead of running a
+// 16-gate tail.  Moved gates may move again from their new level.
+// TFHE_CIRCUIT_PACK=0 turns packing off (A/B runs and tests).
+static void pack_levels(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
+                        const uint32_t *in_b, std::vector<uint32_t> &level,
+                        std::vector<std::vector<uint32_t>> &bs) {
+    const size_t W = n_inputs + n_gates;
+    const uint32_t max_level = (uint32_t)bs.size() - 1;
+    // earliest level among each wire's bootstrapped consumers; NOT consumers pin it
+    constexpr uint32_t PINNED = 0, FREE = 0xFFFFFFFFu;
+    // (kept from the ASAP levels: moving a gate later only raises its inputs'
+    // true first use, so the values stay safe)
+    std::vector<uint32_t> first_use(W, FREE);
+    for (size_t g = 0; g < n_gates; g++) {
+        const bool two = ops[g] <= TFHE_GATE_ORYN;
+        for (int k = 0; k < (two ? 2 : 1); k++) {
+            const uint32_t src = k ? in_b[g] : in_a[g];
+            if (ops[g] == TFHE_GATE_NOT) first_use[src] = PINNED;
+            else if (first_use[src] != PINNED) first_use[src] = std::min(first_use[src], level[n_inputs + g]);
+        }
+    }
+    const size_t R = blind_rotate_round();
+    const size_t J = (512 + R / 4 - 1) / (R / 4) + 1;  // tail breakpoints per round (multiples of #CUs)
+    std::vector<uint32_t> cand;
+    for (uint32_t lv = 1; lv < max_level; lv++) {
+        cand.clear();
+        for (uint32_t g : bs[lv]) {
+            const uint32_t u = first_use[n_inputs + g];
+            if (u != PINNED && (u == FREE || u >= lv + 2)) cand.push_back(g);
+        }
+        if (cand.empty()) continue;
+        const size_t c0 = bs[lv].size(), c1 = bs[lv + 1].size(), k = cand.size();
+        // blind_rotate_cost(c0 - d) only drops where c0 - d reaches a breakpoint
+        // m*R + j*#CUs, so those d (and d = 0) are the only candidates
+        size_t best_d = 0;
+        double best = blind_rotate_cost(c0) + blind_rotate_cost(c1);
+        for (size_t m = (c0 - k) / R; m <= c0 / R; m++)
+            for (size_t j = 0; j <= J; j++) {
+                const size_t bp = m * R + j * (R / 4);
+                if (bp > c0 || bp + k < c0) continue;
+                const size_t d = c0 - bp;
+                const double cost = blind_rotate_cost(bp) + blind_rotate_cost(c1 + d);
+                if (cost < best - 1e-9 || (cost < best + 1e-9 && d < best_d)) {
+                    best = cost;
+                    best_d = d;
+                }
+            }
+        if (best_d == 0) continue;
+        // move the last best_d candidates (those of the latest gates); their
+        // consumers are at lv + 2 or later, their inputs only gain slack
+        for (size_t x = k - best_d; x < k; x++) {
+            level[n_inputs + cand[x]] = lv + 1;
+            bs[lv + 1].push_back(cand[x]);
+        }
+        std::vector<uint32_t> keep;
+        keep.reserve(c0 - best_d);
+        for (uint32_t g : bs[lv])
+            if (level[n_inputs + g] == lv) keep.push_back(g);
+        bs[lv].swap(keep);
+    }
+}
+
 // Wire w < n_inputs is input w; gate g drives wire n_inputs + g.  A
 // bootstrapped gate is ready one level after the later of its inputs; a NOT
 // (negation) is ready with its input.  The device wire table is laid out in
@@ -850,6 +918,8 @@ int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inpu
         const uint32_t lv = ready[n_inputs + g];
         (ops[g] == TFHE_GATE_NOT ? nots[lv] : bs[lv]).push_back((uint32_t)g);
     }
+    const char *pack_e = getenv("TFHE_CIRCUIT_PACK");
+    if (max_level > 1 && !(pack_e && pack_e[0] == '0')) pack_levels(n_inputs, n_gates, ops, in_a, in_b, ready, bs);
     std::vector<uint32_t> slot(W);
     for (size_t w = 0; w < n_inputs; w++) slot[w] = (uint32_t)w;
     uint32_t next = (uint32_t)n_inputs;

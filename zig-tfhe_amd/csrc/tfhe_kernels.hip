@@ -1662,6 +1662,31 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
 // 10,256 gates: 99 vs 106 ms).
 constexpr size_t BR_TAIL_WIDE_MAX = BR_WIDE_MAX_ITEMS;
 
+static size_t device_cus() {
+    static int cus = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return v > 0 ? v : 256;
+    }();
+    return (size_t)cus;
+}
+
+size_t blind_rotate_round() { return (size_t)BR_WAVES * device_cus(); }
+
+// Modelled time of launch_blind_rotate(B) in whole-form rounds, following its
+// dispatch: the latency form takes ~0.43 of a round per item per CU
+// (4.1 ms for up to 256 items, 8.1 ms for 512, a round 9.6 ms).
+double blind_rotate_cost(size_t B) {
+    if (B == 0) return 0.0;
+    const size_t cus = device_cus(), round = BR_WAVES * cus;
+    auto wide = [&](size_t b) { return 0.43 * (double)((b + cus - 1) / cus); };
+    if (B <= BR_WIDE_MAX_ITEMS) return wide(B);
+    const size_t tail = B % round;
+    if (tail == 0 || tail > BR_TAIL_WIDE_MAX || B < round) return (double)((B + round - 1) / round);
+    return (double)(B / round) + wide(tail);
+}
+
 hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
@@ -1673,13 +1698,7 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f);
     }
     if (B <= BR_WIDE_MAX_ITEMS) return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 0);
-    static int cus = [] {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 256;
-        return v > 0 ? v : 256;
-    }();
-    const size_t round = (size_t)BR_WAVES * cus, tail = B % round;
+    const size_t round = blind_rotate_round(), tail = B % round;
     if (tail == 0 || tail > BR_TAIL_WIDE_MAX || B < round)
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'w');
     const size_t main = B - tail;
