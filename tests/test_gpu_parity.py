@@ -93,11 +93,13 @@ def test_key_switch_vs_oracle(oracle, pname, B, form, monkeypatch):
 
 
 # ---- blind rotation / bootstrap ---------------------------------------------
-@pytest.mark.parametrize("form", ["whole", "split", "wide"])
+@pytest.mark.parametrize("form", ["whole", "whole-noloader", "split", "wide"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
 def test_blind_rotate_vs_oracle(oracle, pname, B, form, monkeypatch):
-    """All kernel forms (1 wave per item / 2 waves per item / 8 waves per item) bit-exact."""
-    monkeypatch.setenv("TFHE_BR_KERNEL", form)
+    """All kernel forms (1 wave per item with or without loader waves / 2 waves
+    per item / 8 waves per item) bit-exact."""
+    monkeypatch.setenv("TFHE_BR_KERNEL", form.split("-")[0])
+    monkeypatch.setenv("TFHE_BR_LOADER", "0" if form.endswith("noloader") else "1")
     c, k = ctx_for(oracle, pname)
     cts = u32rand(rng(6), B, k.p.n + 1)  # uniform TLWE: bit-exactness only
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])

@@ -627,7 +627,7 @@ DEV void issue_bk_pair_async(const double2 *__restrict__ src, double2 *slot, int
     }
 }
 
-template <int L>
+template <int L, bool LOADER>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
                   PhaseProf &pp) {
@@ -654,7 +654,8 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #endif
         pp.mark(7);
 #ifndef TFHE_KO_DMA
-        if (rp + 1 < L || has_next) issue_bk_pair_async(next_pair + (size_t)rp * 2048, s_bk + (slot ^ 1) * 2048, tid);
+        if (!LOADER && (rp + 1 < L || has_next))
+            issue_bk_pair_async(next_pair + (size_t)rp * 2048, s_bk + (slot ^ 1) * 2048, tid);
 #endif
         pp.mark(3);
 #ifndef TFHE_KO_MAC
@@ -666,8 +667,11 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
     }
 }
 
-template <int L, bool SMALL>
-__global__ __launch_bounds__(256, 1) void k_blind_rotate(
+// LOADER: 4 more waves per workgroup, one beside each gate's wave on its SIMD,
+// issue the BK row-pair DMAs (the same pieces, slots and barriers), so the
+// gate waves only compute.
+template <int L, bool SMALL, bool LOADER = false>
+__global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
     const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
@@ -677,6 +681,26 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     const int t = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     double2 *s_bk = reinterpret_cast<double2 *>(smem);
+    if constexpr (LOADER) {
+        if (w >= BR_WAVES) {  // loader wave: one barrier per row pair, like the gate waves
+            const int ltid = tid - 64 * BR_WAVES;
+            const size_t stride = (size_t)L * 2048;
+            issue_bk_pair_async(bkd, s_bk, ltid);  // pair (0, 0) into slot 0
+            __syncthreads();                       // the gate waves' prologue barrier
+            for (int i = 0; i < P.n; i++) {
+#pragma unroll 1
+                for (int rp = 0; rp < L; rp++) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces landed
+                    __syncthreads();  // pair published; every gate wave is done with the other slot
+                    const int slot = ((L * i) + rp) & 1;
+                    if (rp + 1 < L || i + 1 < P.n)
+                        issue_bk_pair_async(bkd + (size_t)i * stride + (size_t)(rp + 1) * 2048, s_bk + (slot ^ 1) * 2048,
+                                            ltid);
+                }
+            }
+            return;
+        }
+    }
     C2 *s_tw = reinterpret_cast<C2 *>(smem + BR_LDS_BK);
     C2 *s_twist = reinterpret_cast<C2 *>(smem + BR_LDS_BK + BR_LDS_TW);
     unsigned char *wbase = smem + BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;
@@ -695,7 +719,7 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
     const int op = ops ? (int)ops[g] : 255;
     const size_t step_stride = (size_t)L * 2048;  // double2 per TRGSW (BK[i])
 
-    issue_bk_pair(bkd, s_bk, tid);  // pair (0, 0), lands under the prologue
+    if (!LOADER) issue_bk_pair(bkd, s_bk, tid);  // pair (0, 0), lands under the prologue
     for (int x = tid; x < 511; x += 256) s_tw[x] = TT.tw[x];
     for (int x = tid; x < 512; x += 256) s_twist[x] = TT.twist[x];
 
@@ -768,7 +792,7 @@ __global__ __launch_bounds__(256, 1) void k_blind_rotate(
         wave_sync();
         C2 fa[8], fb[8];
         at_next = s_at[i + 1 < n ? i + 1 : i];
-        br_pairs<L>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
+        br_pairs<L, LOADER>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
                     bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp);
         pp.mark(5);
         inverse_and_add<SMALL, 64, true>(fa, fb, s_x, T, twist_t, t, accA, accB);
@@ -1620,6 +1644,9 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     const bool split = forced == 's';
     // latency form for batches below one gate per SIMD pair
     const bool wide = forced ? forced == 'W' : B <= BR_WIDE_MAX_ITEMS;
+    // whole form: with loader waves unless TFHE_BR_LOADER=0 (A/B runs and tests)
+    const char *loader_e = getenv("TFHE_BR_LOADER");
+    const bool loader = !wide && !split && !(loader_e && loader_e[0] == '0');
     dim3 grid, block;
     if (wide) {
         grid = dim3((unsigned)B);
@@ -1629,7 +1656,7 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
         block = dim3(64 * BS_WAVES);
     } else {
         grid = dim3((unsigned)((B + BR_WAVES - 1) / BR_WAVES));
-        block = dim3(64 * BR_WAVES);
+        block = dim3(64 * BR_WAVES * (loader ? 2 : 1));
     }
 #define BR_LAUNCH(L_, S_)                                                                                         \
     do {                                                                                                          \
@@ -1638,6 +1665,9 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
                                testvec, bk2, out, out_mode, B);                                                   \
         else if (split)                                                                                           \
             hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
+                               testvec, bk2, out, out_mode, B);                                                   \
+        else if (loader)                                                                                          \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
                                testvec, bk2, out, out_mode, B);                                                   \
         else                                                                                                      \
             hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,  \
