@@ -161,6 +161,13 @@ int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *in
                           const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
                           const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels);
 
+/* The schedule tfhe_gpu_circuit_eval runs, host only (no device): levels[g]
+ * = the level gate g runs at (NOT: the level of its input), *depth (may be
+ * NULL) = the bootstrap depth, for a device with `cus` compute units (256 on
+ * the MI355X), with round packing when pack != 0. */
+int tfhe_circuit_schedule(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
+                          const uint32_t *in_b, uint32_t cus, int pack, uint32_t *levels, uint32_t *depth);
+
 /* ---- Proxy re-encryption (proxy_reenc.zig) -------------
  * reencryptTLWELv0 is the identity key switch over a TLWELv0 input (n
  * coefficients instead of N), so it runs on the same lane-per-item kernel.

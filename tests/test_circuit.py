@@ -190,3 +190,91 @@ def test_circuit_round_packing(oracle, monkeypatch):
     print(f"packed {t_pack * 1e3:.1f} ms, unpacked {t_plain * 1e3:.1f} ms")
     assert t_pack < 0.9 * t_plain
     ctx.close()
+
+
+def _check_schedule(c, levels):
+    """Every gate after its inputs (NOT: with its input), in wire terms."""
+    wl = [0] * c.n_inputs + [int(x) for x in levels]
+    for g, (op, a, b) in enumerate(zip(c.ops, c.ia, c.ib)):
+        w = c.n_inputs + g
+        if op == tfhe_amd.NOT:
+            assert wl[w] == wl[a]
+        else:
+            assert wl[w] >= wl[a] + 1
+            if op != tfhe_amd.COPY:
+                assert wl[w] >= wl[b] + 1
+
+
+def test_circuit_schedule_round_packing_host():
+    """tfhe_circuit_schedule (host only): the 1,064-gate level of
+    test_circuit_round_packing hands its 40 output-only gates to level 2 on a
+    256-CU device (one 1,024-gate round), keeps them without packing, and the
+    depth stays 2."""
+    g = np.random.default_rng(12)
+    c = Circuit()
+    ins = [c.input() for _ in range(40)]
+    pairs = g.integers(0, 40, (1064, 2))
+    lvl1 = [c.and_(ins[x], ins[y]) if i % 2 else c.xor(ins[x], ins[y]) for i, (x, y) in enumerate(pairs)]
+    for i in range(0, 200, 2):
+        c.or_(lvl1[i], lvl1[i + 1])
+    plain, d0 = c.schedule(256, pack=False)
+    packed, d1 = c.schedule(256, pack=True)
+    assert d0 == d1 == 2
+    assert np.bincount(plain, minlength=3)[1:].tolist() == [1064, 100]
+    assert np.bincount(packed, minlength=3)[1:].tolist() == [1024, 140]
+    assert (packed[1024:1064] == 2).all() and (packed[:1024] == 1).all()
+    _check_schedule(c, packed)
+    # a 64-CU device: rounds of 256 gates, 1,064 = 4 rounds + a 40-gate tail
+    # (one latency-form pass); moving the 40 would make level 2's 140 gates take
+    # three latency-form passes instead of two: a tie, so nothing moves
+    p64, _ = c.schedule(64)
+    assert np.array_equal(p64, plain)
+
+
+def test_circuit_schedule_mixed_config4_host():
+    """BASELINE config 4 (ops uniform over AND/OR/XOR/MUX, MUX = 3 bootstraps in
+    2 levels): packing leaves level 1 a whole number of 1,024-gate rounds."""
+    g = np.random.default_rng(4)
+    c = Circuit()
+    ins = [c.input() for _ in range(64)]
+    for k in g.integers(0, 4, 8192):
+        a, b, s = (ins[int(x)] for x in g.integers(0, 64, 3))
+        c.output([c.and_, c.or_, c.xor][k](a, b) if k < 3 else c.mux(s, a, b))
+    plain, d0 = c.schedule(256, pack=False)
+    packed, d1 = c.schedule(256, pack=True)
+    assert d0 == d1 == 2
+    boot = np.array([op != tfhe_amd.NOT for op in c.ops])
+    assert int((packed[boot] == 1).sum()) % 1024 == 0
+    assert int((plain[boot] == 1).sum()) % 1024 != 0
+    _check_schedule(c, packed)
+
+
+def test_circuit_schedule_random_dags_host():
+    """Random DAGs with NOT and COPY: packing keeps every dependency and the depth."""
+    g = np.random.default_rng(7)
+    for _ in range(20):
+        c = Circuit()
+        wires = [c.input() for _ in range(8)]
+        for _ in range(int(g.integers(50, 3000))):
+            a, b = (wires[int(x)] for x in g.integers(0, len(wires), 2))
+            r = g.random()
+            wires.append(c.not_(a) if r < 0.1 else c.copy(a) if r < 0.15 else c.nand(a, b))
+        c.output(*wires[-5:])
+        for cus in (4, 64, 256):
+            _, d0 = c.schedule(cus, pack=False)
+            packed, d1 = c.schedule(cus, pack=True)
+            assert d0 == d1
+            assert packed.max(initial=0) <= d0
+            _check_schedule(c, packed)
+
+
+def test_circuit_schedule_rejects_bad_graphs_host():
+    c = Circuit()
+    a = c.input()
+    c.ops.append(77)  # unknown op
+    c.ia.append(a)
+    c.ib.append(a)
+    with pytest.raises(tfhe_amd.TfheError):
+        c.schedule()
+    with pytest.raises(tfhe_amd.TfheError):
+        Circuit().schedule(cus=0)

@@ -822,7 +822,7 @@ int tfhe_reenc_key_gen_asymmetric(const tfhe_params *p, const uint32_t *key_from
 // 16-gate tail.  Moved gates may move again from their new level.
 // TFHE_CIRCUIT_PACK=0 turns packing off (A/B runs and tests).
 static void pack_levels(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
-                        const uint32_t *in_b, std::vector<uint32_t> &level,
+                        const uint32_t *in_b, size_t cus, std::vector<uint32_t> &level,
                         std::vector<std::vector<uint32_t>> &bs) {
     const size_t W = n_inputs + n_gates;
     const uint32_t max_level = (uint32_t)bs.size() - 1;
@@ -839,8 +839,9 @@ static void pack_levels(size_t n_inputs, size_t n_gates, const uint8_t *ops, con
             else if (first_use[src] != PINNED) first_use[src] = std::min(first_use[src], level[n_inputs + g]);
         }
     }
-    const size_t R = blind_rotate_round();
-    const size_t J = (512 + R / 4 - 1) / (R / 4) + 1;  // tail breakpoints per round (multiples of #CUs)
+    const size_t R = 4 * cus;
+    const size_t J = (512 + cus - 1) / cus + 1;  // tail breakpoints per round (multiples of #CUs)
+    auto cost = [&](size_t b) { return blind_rotate_cost(b, cus); };
     std::vector<uint32_t> cand;
     for (uint32_t lv = 1; lv < max_level; lv++) {
         cand.clear();
@@ -853,15 +854,15 @@ static void pack_levels(size_t n_inputs, size_t n_gates, const uint8_t *ops, con
         // blind_rotate_cost(c0 - d) only drops where c0 - d reaches a breakpoint
         // m*R + j*#CUs, so those d (and d = 0) are the only candidates
         size_t best_d = 0;
-        double best = blind_rotate_cost(c0) + blind_rotate_cost(c1);
+        double best = cost(c0) + cost(c1);
         for (size_t m = (c0 - k) / R; m <= c0 / R; m++)
             for (size_t j = 0; j <= J; j++) {
-                const size_t bp = m * R + j * (R / 4);
+                const size_t bp = m * R + j * cus;
                 if (bp > c0 || bp + k < c0) continue;
                 const size_t d = c0 - bp;
-                const double cost = blind_rotate_cost(bp) + blind_rotate_cost(c1 + d);
-                if (cost < best - 1e-9 || (cost < best + 1e-9 && d < best_d)) {
-                    best = cost;
+                const double cd = cost(bp) + cost(c1 + d);
+                if (cd < best - 1e-9 || (cd < best + 1e-9 && d < best_d)) {
+                    best = cd;
                     best_d = d;
                 }
             }
@@ -882,7 +883,54 @@ static void pack_levels(size_t n_inputs, size_t n_gates, const uint8_t *ops, con
 
 // Wire w < n_inputs is input w; gate g drives wire n_inputs + g.  A
 // bootstrapped gate is ready one level after the later of its inputs; a NOT
-// (negation) is ready with its input.  The device wire table is laid out in
+// (negation) is ready with its input.  Fills level[] (per wire), the depth and
+// the bootstrapped / NOT gates of every level (packed unless `pack` is false);
+// returns nullptr, or the reason the graph is invalid.
+static const char *schedule_levels(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
+                                   const uint32_t *in_b, bool pack, size_t cus, std::vector<uint32_t> &level,
+                                   uint32_t &max_level, std::vector<std::vector<uint32_t>> &bs,
+                                   std::vector<std::vector<uint32_t>> &nots) {
+    level.assign(n_inputs + n_gates, 0);
+    max_level = 0;
+    for (size_t g = 0; g < n_gates; g++) {
+        const size_t w = n_inputs + g;
+        const int op = ops[g];
+        const bool bootstrapped = op <= TFHE_GATE_ORYN || op == TFHE_GATE_COPY;
+        if (!bootstrapped && op != TFHE_GATE_NOT) return "unknown gate op";
+        if (in_a[g] >= w) return "gate input a is not an earlier wire";
+        const bool two = op <= TFHE_GATE_ORYN;
+        if (two && in_b[g] >= w) return "gate input b is not an earlier wire";
+        uint32_t r = level[in_a[g]];
+        if (two) r = std::max(r, level[in_b[g]]);
+        level[w] = bootstrapped ? r + 1 : r;
+        max_level = std::max(max_level, level[w]);
+    }
+    // groups in evaluation order: NOT(0), BS(1), NOT(1), ..., BS(max), NOT(max)
+    bs.assign(max_level + 1, {});
+    nots.assign(max_level + 1, {});
+    for (size_t g = 0; g < n_gates; g++) {
+        const uint32_t lv = level[n_inputs + g];
+        (ops[g] == TFHE_GATE_NOT ? nots[lv] : bs[lv]).push_back((uint32_t)g);
+    }
+    if (pack && max_level > 1) pack_levels(n_inputs, n_gates, ops, in_a, in_b, cus, level, bs);
+    return nullptr;
+}
+
+int tfhe_circuit_schedule(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
+                          const uint32_t *in_b, uint32_t cus, int pack, uint32_t *levels, uint32_t *depth) {
+    if ((n_gates && (!ops || !in_a || !in_b || !levels)) || cus == 0) return TFHE_ERR_INVALID;
+    if (n_inputs + n_gates > 0xFFFFFFFFull) return TFHE_ERR_INVALID;
+    std::vector<uint32_t> level;
+    std::vector<std::vector<uint32_t>> bs, nots;
+    uint32_t max_level = 0;
+    if (schedule_levels(n_inputs, n_gates, ops, in_a, in_b, pack != 0, cus, level, max_level, bs, nots))
+        return TFHE_ERR_INVALID;
+    for (size_t g = 0; g < n_gates; g++) levels[g] = level[n_inputs + g];
+    if (depth) *depth = max_level;
+    return TFHE_OK;
+}
+
+// The device wire table is laid out in
 // evaluation order — inputs | NOTs of level 0 | gates of level 1 | NOTs of
 // level 1 | ... — so each level's batch writes one contiguous run of slots,
 // and its inputs are gathered by index inside the blind-rotation prologue.
@@ -894,32 +942,16 @@ int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inpu
     if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
     const size_t W = n_inputs + n_gates, w1 = tlwe0_words(c);
     if (W > 0xFFFFFFFFull) return fail(c, TFHE_ERR_INVALID, "too many wires");
-    // levels
-    std::vector<uint32_t> ready(W, 0);
+    std::vector<uint32_t> ready;
+    std::vector<std::vector<uint32_t>> bs, nots;
     uint32_t max_level = 0;
-    for (size_t g = 0; g < n_gates; g++) {
-        const size_t w = n_inputs + g;
-        const int op = ops[g];
-        const bool bootstrapped = op <= TFHE_GATE_ORYN || op == TFHE_GATE_COPY;
-        if (!bootstrapped && op != TFHE_GATE_NOT) return fail(c, TFHE_ERR_INVALID, "unknown gate op");
-        if (in_a[g] >= w) return fail(c, TFHE_ERR_INVALID, "gate input a is not an earlier wire");
-        const bool two = op <= TFHE_GATE_ORYN;
-        if (two && in_b[g] >= w) return fail(c, TFHE_ERR_INVALID, "gate input b is not an earlier wire");
-        uint32_t r = ready[in_a[g]];
-        if (two) r = std::max(r, ready[in_b[g]]);
-        ready[w] = bootstrapped ? r + 1 : r;
-        max_level = std::max(max_level, ready[w]);
-    }
+    const char *pack_e = getenv("TFHE_CIRCUIT_PACK");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (const char *why = schedule_levels(n_inputs, n_gates, ops, in_a, in_b, !(pack_e && pack_e[0] == '0'),
+                                          device_cus(), ready, max_level, bs, nots))
+        return fail(c, TFHE_ERR_INVALID, why);
     for (size_t o = 0; o < n_outputs; o++)
         if (out_wires[o] >= W) return fail(c, TFHE_ERR_INVALID, "output wire out of range");
-    // groups in evaluation order: NOT(0), BS(1), NOT(1), ..., BS(max), NOT(max)
-    std::vector<std::vector<uint32_t>> bs(max_level + 1), nots(max_level + 1);
-    for (size_t g = 0; g < n_gates; g++) {
-        const uint32_t lv = ready[n_inputs + g];
-        (ops[g] == TFHE_GATE_NOT ? nots[lv] : bs[lv]).push_back((uint32_t)g);
-    }
-    const char *pack_e = getenv("TFHE_CIRCUIT_PACK");
-    if (max_level > 1 && !(pack_e && pack_e[0] == '0')) pack_levels(n_inputs, n_gates, ops, in_a, in_b, ready, bs);
     std::vector<uint32_t> slot(W);
     for (size_t w = 0; w < n_inputs; w++) slot[w] = (uint32_t)w;
     uint32_t next = (uint32_t)n_inputs;

@@ -53,10 +53,11 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out,
                                int out_mode, size_t B, hipStream_t s);
-// items per whole-form round (4 x #CUs) and launch_blind_rotate's modelled time
-// for B items, in rounds (the circuit scheduler's level packing)
-size_t blind_rotate_round();
-double blind_rotate_cost(size_t B);
+// CUs of the current device (256 when it cannot be queried) and
+// launch_blind_rotate's modelled time for B items on `cus` CUs, in whole-form
+// rounds of 4 x cus items (the circuit scheduler's level packing)
+size_t device_cus();
+double blind_rotate_cost(size_t B, size_t cus);
 // dst[k] = (negate ? -1 : 1) * src[idx[k]] for k < count, n+1 words each
 // (TLWELv0.neg: gates.zig:132-135)
 hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint32_t *idx, uint32_t *dst,

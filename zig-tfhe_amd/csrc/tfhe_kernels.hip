@@ -1692,7 +1692,7 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
 // 10,256 gates: 99 vs 106 ms).
 constexpr size_t BR_TAIL_WIDE_MAX = BR_WIDE_MAX_ITEMS;
 
-static size_t device_cus() {
+size_t device_cus() {
     static int cus = [] {
         int dev = 0, v = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1702,14 +1702,13 @@ static size_t device_cus() {
     return (size_t)cus;
 }
 
-size_t blind_rotate_round() { return (size_t)BR_WAVES * device_cus(); }
-
-// Modelled time of launch_blind_rotate(B) in whole-form rounds, following its
-// dispatch: the latency form takes ~0.43 of a round per item per CU
-// (4.1 ms for up to 256 items, 8.1 ms for 512, a round 9.6 ms).
-double blind_rotate_cost(size_t B) {
+// Modelled time of launch_blind_rotate(B) on a device with `cus` CUs, in
+// whole-form rounds (BR_WAVES x cus items), following its dispatch: the
+// latency form takes ~0.43 of a round per item per CU (4.1 ms
+// for up to 256 items, 8.1 ms for 512, a round 9.6 ms).
+double blind_rotate_cost(size_t B, size_t cus) {
     if (B == 0) return 0.0;
-    const size_t cus = device_cus(), round = BR_WAVES * cus;
+    const size_t round = BR_WAVES * cus;
     auto wide = [&](size_t b) { return 0.43 * (double)((b + cus - 1) / cus); };
     if (B <= BR_WIDE_MAX_ITEMS) return wide(B);
     const size_t tail = B % round;
@@ -1728,7 +1727,7 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f);
     }
     if (B <= BR_WIDE_MAX_ITEMS) return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 0);
-    const size_t round = blind_rotate_round(), tail = B % round;
+    const size_t round = BR_WAVES * device_cus(), tail = B % round;
     if (tail == 0 || tail > BR_TAIL_WIDE_MAX || B < round)
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'w');
     const size_t main = B - tail;

@@ -89,6 +89,8 @@ _SIGS = {
     "tfhe_gpu_gate_batch": (C.c_int, [vp, u8p, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_circuit_eval": (C.c_int, [vp, C.c_size_t, u32p, C.c_size_t, u8p, u32p, u32p, C.c_size_t, u32p, u32p,
                                         C.POINTER(C.c_uint32)]),
+    "tfhe_circuit_schedule": (C.c_int, [C.c_size_t, C.c_size_t, u8p, u32p, u32p, C.c_uint32, C.c_int, u32p,
+                                        C.POINTER(C.c_uint32)]),
     "tfhe_gpu_blind_rotate_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_bootstrap_lut_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_gate_batch_dev": (C.c_int, [vp, vp, vp, vp, vp, C.c_size_t]),
@@ -737,6 +739,21 @@ class Circuit:
 
     def output(self, *wires):
         self.outputs.extend(wires)
+
+    def schedule(self, cus: int = 256, pack: bool = True):
+        """The level of every gate as tfhe_gpu_circuit_eval runs it on a device
+        with `cus` CUs (host only, tfhe_circuit_schedule) -> (levels, depth)."""
+        lib = load_library()
+        ops = np.array(self.ops, np.uint8)
+        ia, iap = _u32(np.array(self.ia, np.uint32))
+        ib, ibp = _u32(np.array(self.ib, np.uint32))
+        levels = np.zeros(max(len(self.ops), 1), np.uint32)
+        depth = C.c_uint32(0)
+        rc = lib.tfhe_circuit_schedule(self.n_inputs, ops.size, ops.ctypes.data_as(u8p), iap, ibp, cus, int(pack),
+                                       levels.ctypes.data_as(u32p), C.byref(depth))
+        if rc:
+            raise TfheError(f"circuit_schedule: status {rc}")
+        return levels[:ops.size], depth.value
 
     def run(self, ctx: "Context", inputs):
         inputs = np.asarray(inputs, np.uint32).reshape(-1, ctx.params.n + 1)
