@@ -133,7 +133,30 @@ def gates128_vectors():
     print("gates128 sha256", digest)
 
 
+def lut_uint4_vectors():
+    """BASELINE config 5's bits: UINT4 keys from seeds (sk 42, ck 43), the LUT of
+    f(x) = (x + 1) mod 16 (lut/generator.zig:85-135), every message 0..15 encrypted
+    (tlwe.zig:74-88), 820-step blind rotations with the LUT test vector + sample
+    extract + key switch (trgsw.zig:336-400, :471-502): inputs, test vector, outputs and
+    the outputs' sha256 (the 350 MB key is regenerated from the seeds)."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle, params
+    o = Oracle()
+    p = params("uint4")
+    k0, k1 = o.secret_key(p, 42)
+    ck = o.cloud_key(p, 43, k0, k1)
+    msgs = np.arange(16, dtype=np.uint32)
+    tv = o.lut_generate(p.N, 16, (msgs + 1) % 16)
+    cts = np.array([o.encrypt_lwe_message(p.n, int(m), 16, p.alpha_lv0, k0, 27000 + i) for i, m in enumerate(msgs)])
+    out = o.gate_batch(p, np.full(16, 255, np.uint8), cts, cts, ck, testvec=tv, threads=8)
+    digest = hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest()
+    np.savez(os.path.join(HERE, "lut_uint4.npz"), msgs=msgs, cts=cts, testvec=tv, out=out, out_sha256=digest,
+             params="uint4", sk_seed=42, ck_seed=43)
+    print("lut_uint4 sha256", digest)
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["twiddles", "polymul_bigint", "oracle_vectors", "gates128_vectors"]
+    what = sys.argv[1:] or ["twiddles", "polymul_bigint", "oracle_vectors", "gates128_vectors", "lut_uint4_vectors"]
     for name in what:
         globals()[name]()

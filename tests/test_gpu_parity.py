@@ -229,6 +229,16 @@ def test_lut_pbs_uint4(oracle):
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (msgs + 1) % 16)
 
 
+def test_lut_uint4_golden_fixture(oracle):
+    """The committed config-5 fixture (tests/golden/lut_uint4.npz) through
+    tfhe_gpu_bootstrap_lut_batch with the oracle's seeded UINT4 key: bit-identical."""
+    g = np.load(os.path.join(GOLDEN, "lut_uint4.npz"))
+    c, _ = ctx_for(oracle, "uint4")
+    tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (x + 1) % 16)
+    assert np.array_equal(tv, g["testvec"])
+    assert np.array_equal(c.bootstrap_lut_batch(g["cts"], tv), g["out"])
+
+
 def test_keygen_matches_oracle(oracle):
     """tfhe_gpu_keygen (host RNG + device FFTs) == oracle CloudKey.new, bit for bit."""
     p = get_keys(oracle, "80").p

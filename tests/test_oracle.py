@@ -332,3 +332,22 @@ def test_gates128_golden(oracle):
     dec = [oracle.tlwe_decrypt_bool(k.p.n, c, k.k0) for c in out]
     want = [bool(truth[int(o)](int(a), int(b))) for o, a, b in zip(g["ops"], g["bits_a"], g["bits_b"])]
     assert dec == want
+
+
+def test_lut_uint4_golden(oracle):
+    """BASELINE config 5 pinned by a committed fixture (tests/golden/lut_uint4.npz): UINT4
+    keys from seeds 42/43, the LUT of f(x) = (x+1) mod 16, all 16 messages; the oracle
+    reproduces the test vector, the outputs and their sha256, and they decrypt to f(m)."""
+    import hashlib
+    g = np.load(os.path.join(GOLDEN, "lut_uint4.npz"))
+    k = get_keys(oracle, "uint4")
+    msgs = g["msgs"]
+    tv = oracle.lut_generate(k.p.N, 16, (msgs + 1) % 16)
+    assert np.array_equal(tv, g["testvec"])
+    cts = np.array([oracle.encrypt_lwe_message(k.p.n, int(m), 16, k.p.alpha_lv0, k.k0, 27000 + i)
+                    for i, m in enumerate(msgs)])
+    assert np.array_equal(cts, g["cts"])
+    out = oracle.gate_batch(k.p, np.full(16, 255, np.uint8), cts, cts, k.ck, testvec=tv, threads=8)
+    assert hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest() == str(g["out_sha256"])
+    assert np.array_equal(out, g["out"])
+    assert [oracle.decrypt_lwe_message(k.p.n, c, 16, k.k0) for c in out] == [int(m + 1) % 16 for m in msgs]
