@@ -309,6 +309,8 @@ def main():
         achieved = alg / br_avg_s
         f64_rate = f64_ops_per_cmux(p.L) * p.n * B / br_avg_s
         form = "split" if os.environ.get("TFHE_BR_KERNEL", "").startswith("s") else "whole"
+        if form == "whole" and os.environ.get("TFHE_BR_LOADER", "1")[:1] != "0":
+            form = "whole, loader waves"
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_blind_rotate_r01.json")
         if os.path.exists(pmc_path):
