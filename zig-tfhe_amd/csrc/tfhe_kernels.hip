@@ -684,6 +684,10 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     if constexpr (LOADER) {
         if (w >= BR_WAVES) {  // loader wave: one barrier per row pair, like the gate waves
             const int ltid = tid - 64 * BR_WAVES;
+            // top issue priority: a loader wave's DMA issue and barrier arrival
+            // never wait behind its gate wave (9.14 vs 9.19 ms; raising the gate
+            // waves instead cost 6 %, profiles/r01_ab_loader.txt)
+            __builtin_amdgcn_s_setprio(3);
             const size_t stride = (size_t)L * 2048;
             issue_bk_pair_async(bkd, s_bk, ltid);  // pair (0, 0) into slot 0
             __syncthreads();                       // the gate waves' prologue barrier
