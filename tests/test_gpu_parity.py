@@ -184,6 +184,34 @@ def test_nand_batch_1024_128bit(oracle):
     assert np.array_equal(c.gate_batch(np.zeros(64, np.uint8), A[:64], B[:64]), out[:64])
 
 
+@pytest.mark.parametrize("loader", ["1", "0"])
+def test_gate_batch_rounds_and_tail(oracle, loader, monkeypatch):
+    """2,348 mixed gates (80-bit): two whole-form rounds of 1,024 plus a 300-gate tail
+    that launch_blind_rotate hands to the latency form, on the plain (non-gathered)
+    input path whose tail pointers it offsets.  Truth table for all, oracle bits at
+    the round and tail boundaries, with and without loader waves."""
+    monkeypatch.setenv("TFHE_BR_LOADER", loader)
+    c, k = ctx_for(oracle, "80")
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    g = rng(31)
+    n = 2 * 1024 + 300
+    ops = g.integers(0, 10, n).astype(np.uint8)
+    a_bits = g.integers(0, 2, n).astype(np.uint8)
+    b_bits = g.integers(0, 2, n).astype(np.uint8)
+    A = sk.encrypt_bool(a_bits, seed0=31_000)
+    B = sk.encrypt_bool(b_bits, seed0=41_000)
+    out = c.gate_batch(ops, A, B)
+    ab, bb = a_bits.astype(bool), b_bits.astype(bool)
+    want_bits = np.zeros(n, bool)
+    for o in range(10):  # TRUTH below works on numpy bool arrays
+        m = ops == o
+        want_bits[m] = TRUTH[o](ab[m], bb[m])
+    assert np.array_equal(sk.decrypt_bool(out), want_bits)
+    idx = np.array([0, 1023, 1024, 2047, 2048, n - 1])
+    want = oracle.gate_batch(k.p, ops[idx], A[idx], B[idx], k.ck, threads=6)
+    assert np.array_equal(out[idx], want)
+
+
 TRUTH = {0: lambda a, b: ~(a & b), 1: lambda a, b: a | b, 2: lambda a, b: a & b, 3: lambda a, b: a ^ b,
          4: lambda a, b: a ^ b,  # reference xnorGate computes a - 2b + 1/4: decrypts as XOR (test_oracle.py)
          5: lambda a, b: ~(a | b), 6: lambda a, b: ~a & b, 7: lambda a, b: a & ~b, 8: lambda a, b: ~a | b,
