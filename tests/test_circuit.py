@@ -169,11 +169,15 @@ def test_circuit_round_packing(oracle, monkeypatch):
     bits = g.integers(0, 2, 40)
     inputs = sk.encrypt_bool(bits.astype(np.uint8), seed0=901)
 
-    def timed():
+    def timed():  # warm-up, then the faster of two runs
         c.run(ctx, inputs)
-        t0 = time.perf_counter()
-        out, depth = c.run(ctx, inputs)
-        return out, depth, time.perf_counter() - t0
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            out, depth = c.run(ctx, inputs)
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        return out, depth, best
 
     got, depth, t_pack = timed()
     assert depth == 2
