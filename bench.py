@@ -2,12 +2,20 @@
 
 One step = one pass of the hot path over one batch: B NAND gates (128-bit
 params) = linear pre-combination + blind rotation (700 CMUX) + sample extract
-+ identity key switch, inputs already resident in HBM.  One process per GPU
-(torch.distributed.run); per-GPU batch fixed (weak scaling); the cloud key is
-generated on rank 0 and broadcast once over RCCL/xGMI; no collective on the
-data path.  Rank 0 prints one JSON line.
++ identity key switch, inputs already resident in HBM.  One process per GPU;
+per-GPU batch fixed (weak scaling) unless --global-batch splits a fixed total
+(strong scaling); the cloud key is generated on rank 0 and broadcast once over
+RCCL/xGMI; no collective on the data path.  Rank 0 prints one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--params 128]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B | --global-batch G] [--params 128]
+
+--gpus N > 1 without RANK in the environment: this process starts
+`torch.distributed.run --nproc-per-node N` on itself (a child process; this
+one never touches a GPU) and exits with its status, so the plain command and
+the torchrun form give the same line.  --single-process instead drives all N
+devices from one process through the library's multi-device context
+(tfhe_gpu_create_multi: in-library RCCL key broadcast, one host thread per
+device; host-buffer API, so PCIe copies are inside the timed region).
 
 Other BASELINE configs (parity cases; these print their own line, never the
 default one): --workload adder (config 3: 16-bit ripple-carry adder, one
@@ -36,6 +44,16 @@ import tfhe_amd  # noqa: E402
 
 HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md chip table (spec)
 METRIC = "gate-bootstraps/sec (NAND, 128-bit params) at 1/2/4/8 MI355X; % HBM roofline"
+KERNEL_SRC = os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_kernels.hip")
+PMC_PATH = os.path.join(ROOT, "profiles", "pmc_blind_rotate.json")
+REFERENCE_MS_PER_GATE = 37.31  # zig-tfhe's published single-thread gate time (CHANGELOG.md:86)
+
+
+def kernel_source_hash() -> str:
+    """Tag of the kernel build: sha256 of the HIP source the .so is built from
+    (a PMC file measured on another kernel is not reported as this one's)."""
+    import hashlib
+    return hashlib.sha256(open(KERNEL_SRC, "rb").read()).hexdigest()[:16]
 
 
 def algorithmic_bytes_per_gate(p) -> int:
@@ -65,26 +83,47 @@ VALU_F64_PEAK = 256 * 4 * 16 * 2.4e9  # non-FMA f64 ops/s: 256 CUs x 4 SIMD x 16
 VALU_F64_SUSTAINED = 1024 * 64 / 2.01e-9
 
 
+def host_cpu_info() -> dict:
+    """What the CPU baseline ran on: nproc, the affinity set, the cgroup CPU quota, lscpu's model."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core"):
+                info[k.strip().lower().replace("(s)", "s").replace(" ", "_")] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
 def cpu_baseline(p, sk, bk, ksk, A, B, gpu_out, seconds: float):
-    """Oracle (C restatement of zig-tfhe's CPU path, -O3) on the host cores,
-    on a bounded sample of the same workload; also spot-checks GPU bits."""
+    """Oracle (C restatement of zig-tfhe's CPU path, -O3) on the host cores, on a
+    bounded sample of the same workload: one gate per thread on
+    every core of the affinity set, no cap; also the single-thread rate and a
+    spot check of the GPU's bits."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import CloudKeyArrays, Oracle, params
     o = Oracle(fast=True)
     op = params("128")
     ck = CloudKeyArrays(0x82080000, np.concatenate([np.zeros(p.N, np.uint32),
                                                     np.full(p.N, 0x20000000, np.uint32)]), ksk, bk)
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    # parity spot check of the first gates of the GPU batch
-    nchk = min(cores, A.shape[0])
-    want = o.gate_batch(op, np.zeros(nchk, np.uint8), A[:nchk], B[:nchk], ck, threads=cores)
+    info = host_cpu_info()
+    cores = info["affinity"]
+    nchk = min(16, A.shape[0])  # parity spot check of the first gates of the GPU batch
+    want = o.gate_batch(op, np.zeros(nchk, np.uint8), A[:nchk], B[:nchk], ck, threads=nchk)
     spot_ok = bool(np.array_equal(want, gpu_out[:nchk]))
-    # single-thread rate on a few gates, then all cores for ~`seconds`
     t0 = time.perf_counter()
     o.gate_batch(op, np.zeros(2, np.uint8), A[:2], B[:2], ck, threads=1)
     st_rate = 2 / (time.perf_counter() - t0)
-    done, t0 = 0, time.perf_counter()
-    i = 0
+    done, i = 0, 0
+    t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         idx = (np.arange(cores) + i) % A.shape[0]
         o.gate_batch(op, np.zeros(cores, np.uint8), A[idx], B[idx], ck, threads=cores)
@@ -92,9 +131,54 @@ def cpu_baseline(p, sk, bk, ksk, A, B, gpu_out, seconds: float):
         i += cores
     rate = done / (time.perf_counter() - t0)
     return {"value": round(rate, 2), "unit": "gate-bootstraps/s", "cores": cores, "kind": "port",
-            "sample": (f"{done} NAND gate bootstraps (128-bit) of the same batch, {cores} threads x 1 gate each, "
-                       f"~{seconds:.0f}s; single-thread {st_rate:.2f} gates/s; oracle/tfhe_oracle.c -O3"),
-            "parity_spot_check": {"gates": nchk, "bit_exact": spot_ok}}
+            "sample": (f"{done} NAND gate bootstraps (128-bit) of the same batch, {cores} threads x 1 gate each "
+                       f"(every core of the affinity set), ~{seconds:.0f}s; oracle/tfhe_oracle.c -O3"),
+            "single_thread": {"value": round(st_rate, 2), "ms_per_gate": round(1e3 / st_rate, 2),
+                              "reference_published_ms_per_gate": REFERENCE_MS_PER_GATE},
+            "host": info, "parity_spot_check": {"gates": nchk, "bit_exact": spot_ok}}
+
+
+def pmc_record(batch: int, params: str):
+    """profiles/pmc_blind_rotate.json if it was measured on this kernel source, batch and params."""
+    if not os.path.exists(PMC_PATH):
+        return None, "no PMC file"
+    pmc = json.load(open(PMC_PATH))
+    if pmc.get("kernel_source_sha256") != kernel_source_hash():
+        return None, "PMC file measured on another kernel build (source hash differs): not reported"
+    if pmc.get("batch") != batch or pmc.get("params") != params:
+        return None, "PMC file measured on another batch / parameter set"
+    return pmc, None
+
+
+def rooflines(p, B, params, br_avg_s, kernel):
+    """Primary roofline: f64 VALU issue, the bound the blind rotation is on (its
+    HBM traffic is ~60 GB/s); the SURVEY §8d streamed-key figure beside it."""
+    ops = f64_ops_per_cmux(p.L) * p.n * B
+    f64_rate = ops / br_avg_s
+    pmc, why = pmc_record(B, params)
+    roof = {"bound": "valu_f64", "achieved": round(f64_rate / 1e12, 3), "peak": round(VALU_F64_PEAK / 1e12, 1),
+            "unit": "Tops/s (f64 add+mul, no FMA)", "frac": round(f64_rate / VALU_F64_PEAK, 4),
+            "peak_sustained": round(VALU_F64_SUSTAINED / 1e12, 1),
+            "frac_sustained": round(f64_rate / VALU_F64_SUSTAINED, 4),
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "kernel": kernel, "kernel_avg_ms": round(br_avg_s * 1e3, 3),
+            "algorithmic_f64_ops_per_launch": ops,
+            "f64_ops_per_cmux": f64_ops_per_cmux(p.L)}
+    if pmc:
+        roof["pmc"] = {k: pmc[k] for k in ("valu_f64_insts_per_launch", "valu_insts_per_gate_wave_per_cmux",
+                                           "lds_insts_per_gate_wave_per_cmux", "wait_any_frac_gate_waves")
+                       if k in pmc}
+        if pmc.get("valu_f64_insts_per_launch"):
+            roof["pmc"]["valu_f64_frac_from_pmc"] = round(pmc["valu_f64_insts_per_launch"] * 64 / br_avg_s / VALU_F64_PEAK, 4)
+    else:
+        roof["traffic_note"] = why
+    alg = algorithmic_bytes_per_gate(p) * B
+    hbm = {"bound": "hbm", "achieved": round(alg / br_avg_s / 1e9, 2), "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
+           "frac": round(alg / br_avg_s / HBM_PEAK_BPS, 4), "algorithmic_bytes_per_launch": alg,
+           "note": ("SURVEY §8d streamed-key model: BK bytes every gate consumes (n*2L*2*N*8 + I/O) / kernel time. "
+                    "The 4 gates of a workgroup share each BK row through LDS and the XCDs' L2s hold the key, so "
+                    "this counts key bytes consumed, not DRAM traffic (roofline.traffic is the measured DRAM bytes)")}
+    return roof, hbm
 
 
 def timed(fn, steps, warmup, world, device):
@@ -103,6 +187,7 @@ def timed(fn, steps, warmup, world, device):
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(steps):
         out = fn()
@@ -116,11 +201,20 @@ def timed(fn, steps, warmup, world, device):
     return el, out
 
 
-def run_workload(args, rank, world, device):
-    """Configs 3-5 of BASELINE.json (host-buffer APIs: PCIe copies included)."""
-    pname = "uint4" if args.workload == "lut" else args.params
-    ctx = tfhe_amd.Context(pname, device.index)
-    p = ctx.params
+def per_rank_batch(args, rank, world):
+    """(items on this rank, items over all ranks, scaling): --global-batch G splits
+    G contiguously (strong scaling); else --batch per GPU (weak scaling)."""
+    if args.global_batch:
+        lo, hi = tdist.shard_range(args.global_batch, rank, world)
+        return hi - lo, args.global_batch, "strong"
+    return args.batch, args.batch * world, "weak"
+
+
+def shared_secret_key(ctx, p, rank, world, device):
+    """Rank 0 generates the keys; the cloud key goes to every rank once over RCCL
+    (tfhe_dist.broadcast_cloud_key), the secret key too (test data only: the
+    bench encrypts its synthetic inputs and checks its outputs with it)."""
+    sk = None
     if rank == 0:
         sk, _ = ctx.keygen(42, 43)
     if world > 1:
@@ -131,7 +225,19 @@ def run_workload(args, rank, world, device):
         dist.broadcast(kbuf, 0)
         kk = kbuf.cpu().numpy().astype(np.uint32)
         sk = tfhe_amd.SecretKey(p, kk[:p.n], kk[p.n:])
+    return sk
+
+
+def run_workload(args, rank, world, device):
+    """Configs 3-5 of BASELINE.json (host-buffer APIs: PCIe copies included)."""
+    pname = "uint4" if args.workload == "lut" else args.params
+    ctx = tfhe_amd.Context(pname, device.index)
+    p = ctx.params
+    sk = shared_secret_key(ctx, p, rank, world, device)
+    if args.no_pack:
+        ctx.set_option("circuit_pack", 0)
     g = np.random.default_rng(2000 + rank)
+    B, total, scaling = per_rank_batch(args, rank, world)
     extra = {}
     if args.workload == "adder":
         nadd = args.batch
@@ -156,8 +262,8 @@ def run_workload(args, rank, world, device):
         extra = {"adders_per_step": nadd * world, "gates_per_adder": len(c.ops) // nadd, "levels": depth,
                  "ms_per_adder_circuit": round(el / args.steps * 1e3, 3), "sums_check": ok}
         workload = f"{nadd} independent 16-bit ripple-carry adders per GPU (examples/add_two_numbers.zig), 402+304 first"
+        scaling = "weak"
     elif args.workload == "mixed":
-        B = args.batch
         c = tfhe_amd.Circuit()
         ins = [c.input() for _ in range(3 * B)]
         kinds = g.integers(0, 4, B)
@@ -174,13 +280,13 @@ def run_workload(args, rank, world, device):
         el, (outs, depth) = timed(lambda: c.run(ctx, inputs), args.steps, args.warmup, world, device)
         ok = bool(np.array_equal(sk.decrypt_bool(outs), want))
         n_boot = int(sum(1 for op in c.ops if op != tfhe_amd.NOT))
-        units = B * world * args.steps
+        units = total * args.steps
         metric, unit = "gates/sec (mixed AND/OR/XOR/MUX, 128-bit)", "gates/s"
         extra = {"bootstraps_per_sec": round(n_boot * world * args.steps / el, 2), "levels": depth,
-                 "decrypt_check": ok}
-        workload = f"{B} gates per GPU, op uniform over AND/OR/XOR/MUX (MUX = 3 bootstraps, 2 levels)"
+                 "decrypt_check": ok, "round_packing": not args.no_pack}
+        workload = (f"{total} gates over {world} GPU(s) ({B} on rank 0), op uniform over AND/OR/XOR/MUX "
+                    f"(MUX = 3 bootstraps, 2 levels)")
     elif args.workload == "reenc":
-        B = args.batch
         alice, bob = tfhe_amd.secret_key_new(p, 11), tfhe_amd.secret_key_new(p, 12)
         key = tfhe_amd.ProxyReencryptionKey.new_symmetric(alice, bob, 1000)  # same seeds on every rank
         hr = tfhe_amd.HipReencryptor(ctx, key)
@@ -189,31 +295,92 @@ def run_workload(args, rank, world, device):
         el, outs = timed(lambda: hr.reencrypt(cts), args.steps, args.warmup, world, device)
         ok = bool(np.array_equal(bob.decrypt_bool(outs), bits.astype(bool)))
         hr.close()
-        units = B * world * args.steps
+        units = total * args.steps
         metric, unit = "TLWELv0 proxy re-encryptions/sec", "reencryptions/s"
         extra = {"decrypt_check": ok, "dtype": "u32"}
-        workload = (f"{B} reencryptTLWELv0 per GPU (proxy_reenc.zig:267-306; n={p.n}, basebit {p.basebit}, "
-                    f"t={p.iks_t}; host buffers, PCIe included)")
+        workload = (f"{total} reencryptTLWELv0 over {world} GPU(s) (proxy_reenc.zig:267-306; n={p.n}, "
+                    f"basebit {p.basebit}, t={p.iks_t}; host buffers, PCIe included)")
     else:  # lut
-        B = args.batch
         m = 16
         tv = tfhe_amd.lut_generate(p, m, lambda x: (x * x + 3) % m)
         msgs = g.integers(0, m, B).astype(np.uint32)
         cts = sk.encrypt_lwe_message(msgs, m, seed0=1)
         el, outs = timed(lambda: ctx.bootstrap_lut_batch(cts, tv), args.steps, args.warmup, world, device)
         ok = bool(np.array_equal(sk.decrypt_lwe_message(outs, m), (msgs * msgs + 3) % m))
-        units = B * world * args.steps
+        units = total * args.steps
         metric, unit = "programmable bootstraps/sec (UINT4 LUT)", "bootstraps/s"
         extra = {"decrypt_check": ok}
-        workload = f"{B} UINT4 LUT bootstraps per GPU (f(x) = x^2+3 mod 16; n=820, L=1, Bg=2^22, t=3, basebit 5)"
+        workload = (f"{total} UINT4 LUT bootstraps over {world} GPU(s) (f(x) = x^2+3 mod 16; n=820, L=1, "
+                    f"Bg=2^22, t=3, basebit 5)")
+    ok_all = torch.tensor([0.0 if extra.get("decrypt_check", extra.get("sums_check", True)) else 1.0],
+                          dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(ok_all, op=dist.ReduceOp.MAX)
     if rank == 0:
+        for k in ("decrypt_check", "sums_check"):
+            if k in extra:
+                extra[k] = float(ok_all[0]) == 0.0
         line = {"metric": metric, "value": round(units / el, 2), "unit": unit, "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded keys and inputs)",
-                "config": {"workload": workload, "params": pname, "parallelism": f"dp{world}"}}
+                "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded keys and inputs)",
+                "config": {"workload": workload, "params": pname, "parallelism": f"dp{world}"},
+                "kernels": ctx.last_kernels()}
         line.update(extra)
         print(json.dumps(line), flush=True)
     ctx.close()
+
+
+def run_single_process(args):
+    """All --gpus devices from this one process through tfhe_gpu_create_multi:
+    the library broadcasts the key over RCCL itself and runs one host thread per
+    device.  Host-buffer gate batches (PCIe in the timed region)."""
+    n = args.gpus
+    ctx = tfhe_amd.Context.multi(args.params, num_devices=n)
+    p = ctx.params
+    t0 = time.perf_counter()
+    sk, _ = ctx.keygen(42, 43)
+    keygen_s = time.perf_counter() - t0
+    B = args.global_batch or args.batch * n
+    g = np.random.default_rng(1000)
+    a_bits = g.integers(0, 2, B).astype(np.uint8)
+    b_bits = g.integers(0, 2, B).astype(np.uint8)
+    A = sk.encrypt_bool(a_bits, seed0=1_000_000)
+    Bc = sk.encrypt_bool(b_bits, seed0=5_000_000)
+    ops = np.zeros(B, np.uint8)
+    for _ in range(args.warmup):
+        out = ctx.gate_batch(ops, A, Bc)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = ctx.gate_batch(ops, A, Bc)
+    el = time.perf_counter() - t0
+    ok = bool(np.array_equal(sk.decrypt_bool(out), ~(a_bits.astype(bool) & b_bits.astype(bool))))
+    line = {"metric": METRIC + " [single-process multi-device context, host buffers]", "value": round(B * args.steps / el, 2),
+            "unit": "gate-bootstraps/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: fresh encryptions of uniform random bits under a seeded key (sk 42, ck 43)",
+            "config": {"workload": f"{B} NAND gate bootstraps per step over {n} device(s) of one context "
+                                   f"(tfhe_gpu_create_multi; keygen + RCCL key broadcast {keygen_s:.1f} s, untimed)",
+                       "global_batch": B, "params": args.params, "parallelism": f"dp{n} (one process)"},
+            "kernels": ctx.last_kernels(), "decrypt_check": ok}
+    print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: run `torch.distributed.run` on this script as
+    a child process (this process never initialises a GPU) and return its status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -221,16 +388,27 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1024, help="NAND gates per GPU per step")
+    ap.add_argument("--batch", type=int, default=1024, help="gates per GPU per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="gates per step over all GPUs, split ceil(G/N) per GPU (strong scaling)")
     ap.add_argument("--params", default="128")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives --gpus devices through the library's multi-device context")
+    ap.add_argument("--no-pack", action="store_true", help="mixed/adder: circuit round packing off")
     ap.add_argument("--workload", default="nand", choices=["nand", "adder", "mixed", "lut", "reenc"],
                     help="nand = the headline metric (default); others: BASELINE configs 3-5")
     args = ap.parse_args()
 
+    if args.single_process:
+        return run_single_process(args)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args))
     rank, world, local = tdist.env_rank_world()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: {world} rank(s) launched but --gpus {args.gpus}")
     if world > 1:
         dist.init_process_group(args.dist_backend)  # nccl = RCCL over xGMI
     # one rank per GPU; --dist-backend gloo with more ranks than GPUs only
@@ -259,7 +437,7 @@ def main():
         sk = tfhe_amd.SecretKey(p, kk[:p.n], kk[p.n:])
 
     # synthetic inputs: fresh encryptions of uniform random bits (seed 1000 + rank)
-    B = args.batch
+    B, total, scaling = per_rank_batch(args, rank, world)
     g = np.random.default_rng(1000 + rank)
     a_bits = g.integers(0, 2, B).astype(np.uint8)
     b_bits = g.integers(0, 2, B).astype(np.uint8)
@@ -301,39 +479,23 @@ def main():
     all_correct = float(stats[1]) == 0.0
 
     if rank == 0:
-        total = B * world * args.steps
-        value = total / elapsed
+        value = total * args.steps / elapsed
         br_avg_s = br_ms / 1e3 / max(1, launches)
         ks_avg_s = ks_ms / 1e3 / max(1, launches)
-        alg = algorithmic_bytes_per_gate(p) * B
-        achieved = alg / br_avg_s
-        f64_rate = f64_ops_per_cmux(p.L) * p.n * B / br_avg_s
-        form = "split" if os.environ.get("TFHE_BR_KERNEL", "").startswith("s") else "whole"
-        if form == "whole" and os.environ.get("TFHE_BR_LOADER", "1")[:1] != "0":
-            form = "whole, loader waves"
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_blind_rotate_r01.json")
-        if os.path.exists(pmc_path):
-            pmc = json.load(open(pmc_path))
-            if pmc.get("batch") == B and pmc.get("params") == args.params:
-                traffic = pmc.get("hbm_bytes_per_launch")
+        kernels = ctx.last_kernels()
+        roof, hbm = rooflines(p, B, args.params, br_avg_s, kernels.split(" + ")[0])
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "gate-bootstraps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: fresh encryptions of uniform random bits under a seeded key (sk 42, ck 43)",
             "config": {"workload": f"{B} NAND gate bootstraps per GPU per step, SECURITY_128_BIT "
                                    f"(n={p.n}, N={p.N}, L={p.L}, Bg=2^{p.bgbit}, t={p.iks_t})",
-                       "global_batch": B * world, "params": args.params, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": HBM_PEAK_BPS / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_BPS, 4), "traffic": traffic,
-                         "kernel": f"k_blind_rotate<{p.L}> ({form} form)", "kernel_avg_ms": round(br_avg_s * 1e3, 3),
-                         "algorithmic_bytes_per_launch": alg},
-            "valu_f64": {"achieved": round(f64_rate / 1e12, 2), "peak": round(VALU_F64_PEAK / 1e12, 1),
-                         "unit": "Tops/s (f64 add+mul, no FMA)", "frac": round(f64_rate / VALU_F64_PEAK, 4),
-                         "peak_sustained": round(VALU_F64_SUSTAINED / 1e12, 1),
-                         "frac_sustained": round(f64_rate / VALU_F64_SUSTAINED, 4)},
-            "key_switch_avg_ms": round(ks_avg_s * 1e3, 3),
+                       "global_batch": total, "params": args.params, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "roofline_hbm_accounting": hbm,
+            "key_switch": {"kernel": kernels.split(" + ")[-1], "avg_ms": round(ks_avg_s * 1e3, 3)},
+            "kernel_source_sha256": kernel_source_hash(),
             "decrypt_check": all_correct,
         }
         if want_cpu:

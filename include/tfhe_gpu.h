@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 1
+#define TFHE_GPU_ABI_VERSION 2
 
 enum {
     TFHE_OK = 0,
@@ -74,8 +74,57 @@ int         tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx 
 void        tfhe_gpu_destroy(tfhe_gpu_ctx *ctx);
 const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *ctx);
 int         tfhe_gpu_sync(tfhe_gpu_ctx *ctx);
-/* Run this context's work on a caller-owned hipStream_t (NULL = own stream). */
+/* Run this context's work on a caller-owned hipStream_t (NULL = own stream).
+ * Multi-device context: the stream of its first device. */
 int         tfhe_gpu_set_stream(tfhe_gpu_ctx *ctx, void *hip_stream);
+
+/* ---- Multi-device context (bootstrap.zig:30-47 strategy over
+ * the 8 GPUs of one node) ---------------------------------------------------
+ * One context over `num_devices` HIP devices (`devices` = their ids, NULL =
+ * 0..num_devices-1).  Key loads (load_cloud_key, keygen, the key file and
+ * device-blob imports) land on the first device and are broadcast once to
+ * the others with ncclBroadcast over RCCL (xGMI; librccl is loaded at that
+ * point); a device listed twice (a test of the sharding on one GPU) gets a
+ * device-to-device copy instead.  The host-buffer batch entry points
+ * (bootstrap / gate / blind-rotate / LUT / key-switch / re-encryption) split
+ * the batch into contiguous slices of ceil(B/num_devices) items, one per
+ * device, run them concurrently (one host thread and one stream per device)
+ * and copy each slice's results into the caller's buffer; circuit_eval
+ * places the connected components of the gate DAG on the devices (largest
+ * first, least-loaded device), so no wire crosses a device.  Device-pointer
+ * (_dev) and stage entry points and the profile timers use the first device.
+ * Nothing is exchanged between devices after the key broadcast. */
+int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int *devices, tfhe_gpu_ctx **out);
+int tfhe_gpu_num_devices(const tfhe_gpu_ctx *ctx);
+
+/* ---- Options (kernel forms and table sources; default = the measured-
+ * fastest forms).  Set on a context before use; a multi-device context
+ * passes them to every device.  TFHE_ERR_INVALID for an unknown key or value. */
+enum {
+    TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 2 split, 3 latency */
+    TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
+    TFHE_OPT_KS_FORM = 3,         /* key switch: 0 lanes (default), 1 select / gather */
+    TFHE_OPT_KS_NARROW = 4,       /* basebit 2: 0 auto (default), 1 32-word x 4-wave blocks */
+    TFHE_OPT_KS_ITEM_GROUPS = 5,  /* basebit >= 5: item groups per block, 0 auto (4), 1, 2, 4, 8 */
+    TFHE_OPT_KS_SEL_ITEMS = 6,    /* select / gather form: items per block, 8 (default), 16, 32 */
+    TFHE_OPT_CIRCUIT_PACK = 7,    /* circuit_eval round packing: 1 (default), 0 off */
+    TFHE_OPT_TWIDDLES = 8         /* cos/sin source of the FFT tables: TFHE_TWIDDLES_* (set before a key
+                                     is generated: keygen transforms the key with these tables) */
+};
+/* The two libm candidates a Zig build of the reference can bind @cos/@sin to
+ * (fft.zig:98-106, :591-593): glibc (linkLibC on Linux) or Zig's compiler_rt
+ * port of the fdlibm/musl kernels.  DESIGN.md §6 lists the entries where the
+ * two tables differ. */
+enum { TFHE_TWIDDLES_GLIBC = 0, TFHE_TWIDDLES_FDLIBM = 1 };
+int tfhe_gpu_set_option(tfhe_gpu_ctx *ctx, int key, int64_t value);
+int tfhe_gpu_get_option(const tfhe_gpu_ctx *ctx, int key, int64_t *value);
+/* Names of the kernels the last bootstrap launch of this context ran
+ * ("<blind rotation> + <key switch>"; first device of a multi-device context). */
+const char *tfhe_gpu_last_kernels(tfhe_gpu_ctx *ctx);
+/* The FFT constant tables for N (twist N/2 entries, forward stage twiddles
+ * N/2-1 entries, fft.zig:92-106 and :590-616) from `source`; host only. */
+int tfhe_fft_tables(uint32_t N, int source, double *twist_re, double *twist_im, double *stage_re,
+                    double *stage_im);
 
 /* ---- Cloud key (key.zig:61-118) -------------------------------------- */
 /* Upload a CloudKey held in host memory in the reference layout
@@ -154,7 +203,7 @@ int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, const ui
  * (bootstrapped) or TFHE_GATE_NOT (free).  Each dependency level is one
  * batched bootstrap launch; every wire stays in HBM.  Gates with slack may
  * run one level later than their earliest level when that avoids a ragged
- * partial round (depth unchanged; env TFHE_CIRCUIT_PACK=0 disables it).
+ * partial round (depth unchanged; TFHE_OPT_CIRCUIT_PACK = 0 disables it).
  * outputs receives the n_outputs wires out_wires[]; *levels (may be NULL)
  * the bootstrap depth. */
 int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *inputs, size_t n_gates,

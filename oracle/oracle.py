@@ -86,6 +86,15 @@ class Oracle:
                                                     C.c_uint64, u32p]
         L.oracle_reenc_key_gen.argtypes = [C.c_uint32, u32p, u32p, u32p, C.c_size_t, C.c_double, C.c_uint32,
                                            C.c_uint32, C.c_uint64, u32p]
+        L.oracle_set_trig_source.argtypes = [C.c_int]
+        L.oracle_get_trig_source.restype = C.c_int
+
+    # ---- cos/sin source of the twiddles (0 glibc, 1 fdlibm/musl; tfhe_oracle.c)
+    def set_trig_source(self, source: int):
+        self.lib.oracle_set_trig_source(int(source))
+
+    def trig_source(self) -> int:
+        return self.lib.oracle_get_trig_source()
 
     # ---- utils / fft
     def f64_to_torus(self, d: float) -> int:

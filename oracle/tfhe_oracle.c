@@ -8,7 +8,8 @@
  * expression trees, same loop order, same rounding.  Build with
  * -ffp-contract=off (no FMA contraction): Zig's default float mode is strict
  * and the reference never uses @mulAdd.  Twiddles come from the
- * host libm (glibc) exactly as the reference's @cos/@sin calls.
+ * host libm (glibc) exactly as the reference's @cos/@sin calls,
+ * or from the fdlibm/musl restatement below (oracle_set_trig_source(1)).
  *
  * Paths are relative to the reference root (thedonutfactory/zig-tfhe).
  */
@@ -131,6 +132,107 @@ static uint32_t gaussian_torus(uint32_t mu, normal_dist *nd, oracle_rng *r) {
 }
 
 /* ======================================================================== */
+/* cos/sin of the twiddles: the reference's @cos/@sin (fft.zig:98-106,       */
+/* :591-593) bind to glibc (source 0, this host's libm) or, in a Zig build   */
+/* that keeps compiler_rt's, to its port of the fdlibm/musl kernels (source  */
+/* 1, restated here from musl __cos.c / __sin.c / __rem_pio2.c / cos.c /     */
+/* sin.c for |x| <= 5pi/4 and the medium reduction at ~pi/2, ~pi).  The      */
+/* Box-Muller noise (utils.zig:50-82) keeps glibc in both.                   */
+/* ======================================================================== */
+static double fd_kcos(double x, double y) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
+                 C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double z = x * x, w = z * z;
+    double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    double hz = 0.5 * z;
+    w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+
+static double fd_ksin(double x, double y, int iy) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
+                 S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    double z = x * x, w = z * z;
+    double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
+    double v = z * x;
+    if (iy == 0) return x + v * (S1 + z * r);
+    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+
+static uint64_t f64_bits(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
+
+static int fd_rem_pio2(double x, double *y) {
+    const double toint = 1.5 / 2.220446049250313080847e-16, pio4 = 0x1.921fb54442d18p-1,
+                 invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
+                 pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
+                 pio2_3t = 8.47842766036889956997e-32;
+    uint64_t u = f64_bits(x);
+    int sign = (int)(u >> 63);
+    uint32_t ix = (uint32_t)(u >> 32) & 0x7fffffffu;
+    if (ix <= 0x400f6a7a && (ix & 0xfffff) != 0x921fb) {
+        double k = ix <= 0x4002d97c ? 1.0 : 2.0, z;
+        if (!sign) {
+            z = x - k * pio2_1;
+            y[0] = z - k * pio2_1t;
+            y[1] = (z - y[0]) - k * pio2_1t;
+            return (int)k;
+        }
+        z = x + k * pio2_1;
+        y[0] = z + k * pio2_1t;
+        y[1] = (z - y[0]) + k * pio2_1t;
+        return -(int)k;
+    }
+    double fn = x * invpio2 + toint - toint;
+    int n = (int)fn;
+    double r = x - fn * pio2_1, w = fn * pio2_1t;
+    if (r - w < -pio4) { n--; fn--; r = x - fn * pio2_1; w = fn * pio2_1t; }
+    else if (r - w > pio4) { n++; fn++; r = x - fn * pio2_1; w = fn * pio2_1t; }
+    y[0] = r - w;
+    int ex = (int)(ix >> 20), ey = (int)((f64_bits(y[0]) >> 52) & 0x7ff);
+    if (ex - ey > 16) {
+        double t = r;
+        w = fn * pio2_2; r = t - w; w = fn * pio2_2t - ((t - r) - w); y[0] = r - w;
+        ey = (int)((f64_bits(y[0]) >> 52) & 0x7ff);
+        if (ex - ey > 49) { t = r; w = fn * pio2_3; r = t - w; w = fn * pio2_3t - ((t - r) - w); y[0] = r - w; }
+    }
+    y[1] = (r - y[0]) - w;
+    return n;
+}
+
+static double fd_cos(double x) {
+    uint32_t ix = (uint32_t)(f64_bits(x) >> 32) & 0x7fffffffu;
+    if (ix <= 0x3fe921fb) return ix < 0x3e46a09e ? 1.0 : fd_kcos(x, 0.0);
+    double y[2];
+    switch (fd_rem_pio2(x, y) & 3) {
+    case 0: return fd_kcos(y[0], y[1]);
+    case 1: return -fd_ksin(y[0], y[1], 1);
+    case 2: return -fd_kcos(y[0], y[1]);
+    default: return fd_ksin(y[0], y[1], 1);
+    }
+}
+
+static double fd_sin(double x) {
+    uint32_t ix = (uint32_t)(f64_bits(x) >> 32) & 0x7fffffffu;
+    if (ix <= 0x3fe921fb) return ix < 0x3e500000 ? x : fd_ksin(x, 0.0, 0);
+    double y[2];
+    switch (fd_rem_pio2(x, y) & 3) {
+    case 0: return fd_ksin(y[0], y[1], 1);
+    case 1: return fd_kcos(y[0], y[1]);
+    case 2: return -fd_ksin(y[0], y[1], 1);
+    default: return -fd_kcos(y[0], y[1]);
+    }
+}
+
+static int g_trig_source = 0;  /* oracle_set_trig_source; tests switch it around a call */
+void oracle_set_trig_source(int source) { g_trig_source = source == 1 ? 1 : 0; }
+int oracle_get_trig_source(void) { return g_trig_source; }
+static double tw_cos(double x) { return g_trig_source ? fd_cos(x) : cos(x); }
+static double tw_sin(double x) { return g_trig_source ? fd_sin(x) : sin(x); }
+double oracle_trig_cos(double x, int source) { return source == 1 ? fd_cos(x) : cos(x); }
+double oracle_trig_sin(double x, int source) { return source == 1 ? fd_sin(x) : sin(x); }
+
+/* ======================================================================== */
 /* FFT — fft.zig KlemsaProcessor                                             */
 /* ======================================================================== */
 /* twisties: KlemsaProcessor.new, fft.zig:92-106 */
@@ -138,22 +240,32 @@ void oracle_twist_table(uint32_t N, double *re, double *im) {
     double twist_unit = PI_F64 / (double)N;
     for (uint32_t i = 0; i < N / 2; i++) {
         double angle = (double)i * twist_unit;
-        re[i] = cos(angle);
-        im[i] = sin(angle);
+        re[i] = tw_cos(angle);
+        im[i] = tw_sin(angle);
     }
 }
 
 /* The reference keeps the twist table in its (threadlocal) processor
- * (fft.zig:79-90, :983-992); cache it per N the same way. */
-static pthread_once_t twist_once = PTHREAD_ONCE_INIT;
-static double twist1024_re[512], twist1024_im[512];
-static void twist1024_init(void) { oracle_twist_table(1024, twist1024_re, twist1024_im); }
+ * (fft.zig:79-90, :983-992); cache it per N (and trig source) the same way. */
+static pthread_once_t twist_once[2] = {PTHREAD_ONCE_INIT, PTHREAD_ONCE_INIT};
+static double twist1024_re[2][512], twist1024_im[2][512];
+static void twist_fill(int src) {
+    double twist_unit = PI_F64 / 1024.0;
+    for (uint32_t i = 0; i < 512; i++) {
+        double angle = (double)i * twist_unit;
+        twist1024_re[src][i] = oracle_trig_cos(angle, src);
+        twist1024_im[src][i] = oracle_trig_sin(angle, src);
+    }
+}
+static void twist1024_init0(void) { twist_fill(0); }
+static void twist1024_init1(void) { twist_fill(1); }
 
 static void get_twist(uint32_t N, double *re, double *im) {
     if (N == 1024) {
-        pthread_once(&twist_once, twist1024_init);
-        memcpy(re, twist1024_re, sizeof twist1024_re);
-        memcpy(im, twist1024_im, sizeof twist1024_im);
+        int src = g_trig_source;
+        pthread_once(&twist_once[src], src ? twist1024_init1 : twist1024_init0);
+        memcpy(re, twist1024_re[src], sizeof twist1024_re[src]);
+        memcpy(im, twist1024_im[src], sizeof twist1024_im[src]);
     } else {
         oracle_twist_table(N, re, im);
     }
@@ -176,8 +288,8 @@ static void radix2_fft(cplx *data, size_t n, int inverse) {
     bit_reverse_radix2(data, n);
     for (size_t len = 2; len <= n; len *= 2) {
         double angle = inverse ? 2.0 * PI_F64 / (double)len : -2.0 * PI_F64 / (double)len;
-        double wlen_re = cos(angle);
-        double wlen_im = sin(angle);
+        double wlen_re = tw_cos(angle);
+        double wlen_im = tw_sin(angle);
         for (size_t i = 0; i < n; i += len) {
             double w_re = 1.0, w_im = 0.0;
             for (size_t j = 0; j < len / 2; j++) {
@@ -205,7 +317,7 @@ void oracle_stage_twiddles(uint32_t N, int inverse, double *re, double *im) {
     size_t n = N / 2;
     for (size_t len = 2; len <= n; len *= 2) {
         double angle = inverse ? 2.0 * PI_F64 / (double)len : -2.0 * PI_F64 / (double)len;
-        double wlen_re = cos(angle), wlen_im = sin(angle);
+        double wlen_re = tw_cos(angle), wlen_im = tw_sin(angle);
         double w_re = 1.0, w_im = 0.0;
         for (size_t j = 0; j < len / 2; j++) {
             re[len / 2 - 1 + j] = w_re;

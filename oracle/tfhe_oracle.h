@@ -136,6 +136,13 @@ void oracle_reenc_key_gen(uint32_t n, const uint32_t *key_from, const uint32_t *
                           size_t pk_size, double alpha, uint32_t basebit, uint32_t t, uint64_t seed0,
                           uint32_t *out);
 
+/* cos/sin source of the FFT twiddles: 0 = glibc (default), 1 = the
+ * fdlibm/musl kernels Zig's compiler_rt ports. */
+void oracle_set_trig_source(int source);
+int oracle_get_trig_source(void);
+double oracle_trig_cos(double x, int source);
+double oracle_trig_sin(double x, int source);
+
 #ifdef __cplusplus
 }
 #endif

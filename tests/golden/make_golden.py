@@ -7,7 +7,9 @@ vectors for this path, so the fixtures are of two kinds:
   - twiddles.npz: the reference's twist factors cos/sin(i*pi/1024) (fft.zig:98-106)
     evaluated by the platform libm (glibc, via Python's math module) and
     correctly rounded by mpmath (200 bits); the stage-twiddle recurrence of
-    radix2FFT (fft.zig:590-616) restated in Python floats (IEEE doubles).
+    radix2FFT (fft.zig:590-616) restated in Python floats (IEEE doubles); and
+    the same tables from the fdlibm/musl cos/sin that Zig's compiler_rt ports
+    (fdlibm_trig.py, the `*_fdlibm` arrays), the other libm a Zig build can bind.
   - polymul_bigint.npz: exact negacyclic products mod 2^32 by Python big ints.
 * oracle regression vectors (oracle_vectors.npz): seeded inputs and the
   oracle's outputs for the FFT pair and a small gate batch, so the GPU tests
@@ -23,25 +25,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 
 
-def twiddles():
-    import mpmath
-    mpmath.mp.prec = 200
-    N = 1024
-    unit = math.pi / N
-    re_g, im_g, re_c, im_c = [], [], [], []
-    for i in range(N // 2):
-        ang = float(i) * unit  # one f64 rounding, like the reference
-        re_g.append(math.cos(ang))
-        im_g.append(math.sin(ang))
-        a = mpmath.mpf(ang)
-        re_c.append(float(mpmath.cos(a)))
-        im_c.append(float(mpmath.sin(a)))
+def stage_recurrence(cos, sin, N=1024):
+    """radix2FFT's stage twiddles (fft.zig:590-616): w <- w*wlen per block, restated in Python floats."""
     fr, fi = [0.0] * (N // 2 - 1), [0.0] * (N // 2 - 1)
-    n = N // 2
     ln = 2
-    while ln <= n:
+    while ln <= N // 2:
         ang = -2.0 * math.pi / ln
-        wr, wi = math.cos(ang), math.sin(ang)
+        wr, wi = cos(ang), sin(ang)
         w_re, w_im = 1.0, 0.0
         for j in range(ln // 2):
             fr[ln // 2 - 1 + j], fi[ln // 2 - 1 + j] = w_re, w_im
@@ -49,13 +39,41 @@ def twiddles():
             w_im = w_re * wi + w_im * wr
             w_re = t
         ln *= 2
+    return fr, fi
+
+
+def twiddles():
+    import mpmath
+    sys.path.insert(0, HERE)
+    import fdlibm_trig as fd
+    mpmath.mp.prec = 200
+    N = 1024
+    unit = math.pi / N
+    re_g, im_g, re_c, im_c, re_f, im_f = [], [], [], [], [], []
+    for i in range(N // 2):
+        ang = float(i) * unit  # one f64 rounding, like the reference
+        re_g.append(math.cos(ang))
+        im_g.append(math.sin(ang))
+        re_f.append(fd.cos(ang))
+        im_f.append(fd.sin(ang))
+        a = mpmath.mpf(ang)
+        re_c.append(float(mpmath.cos(a)))
+        im_c.append(float(mpmath.sin(a)))
+    fr, fi = stage_recurrence(math.cos, math.sin, N)
+    fr_f, fi_f = stage_recurrence(fd.cos, fd.sin, N)
     np.savez(os.path.join(HERE, "twiddles.npz"),
              twist_re_glibc=np.array(re_g), twist_im_glibc=np.array(im_g),
              twist_re_cr=np.array(re_c), twist_im_cr=np.array(im_c),
-             stage_fwd_re=np.array(fr), stage_fwd_im=np.array(fi))
-    diff = [(i, "cos") for i in range(N // 2) if re_g[i] != re_c[i]] + \
-           [(i, "sin") for i in range(N // 2) if im_g[i] != im_c[i]]
-    print("twist entries where libm != correctly rounded:", diff)
+             stage_fwd_re=np.array(fr), stage_fwd_im=np.array(fi),
+             twist_re_fdlibm=np.array(re_f), twist_im_fdlibm=np.array(im_f),
+             stage_fwd_re_fdlibm=np.array(fr_f), stage_fwd_im_fdlibm=np.array(fi_f))
+    for name, (r, m) in {"glibc": (re_g, im_g), "fdlibm": (re_f, im_f)}.items():
+        diff = [(i, "cos") for i in range(N // 2) if r[i] != re_c[i]] + \
+               [(i, "sin") for i in range(N // 2) if m[i] != im_c[i]]
+        print(f"twist entries where {name} != correctly rounded:", sorted(diff))
+    print("twist entries glibc != fdlibm:", sorted([(i, "cos") for i in range(N // 2) if re_g[i] != re_f[i]] +
+                                                   [(i, "sin") for i in range(N // 2) if im_g[i] != im_f[i]]))
+    print("stage entries glibc != fdlibm:", [i for i in range(N // 2 - 1) if fr[i] != fr_f[i] or fi[i] != fi_f[i]])
 
 
 def polymul_bigint(count=3):
@@ -133,6 +151,28 @@ def gates128_vectors():
     print("gates128 sha256", digest)
 
 
+def gates128_fdlibm_vectors():
+    """gates128_vectors with the FFT twiddles from the fdlibm/musl cos/sin (the
+    other libm a Zig build can bind): the key is regenerated from
+    the same seeds (its BK transforms use those twiddles too), same inputs."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle, params
+    o = Oracle()
+    o.set_trig_source(1)
+    p = params("128")
+    k0, k1 = o.secret_key(p, 42)
+    ck = o.cloud_key(p, 43, k0, k1)
+    g = np.load(os.path.join(HERE, "gates128.npz"))
+    out = o.gate_batch(p, g["ops"], g["a"], g["b"], ck, threads=8)
+    o.set_trig_source(0)
+    digest = hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest()
+    np.savez(os.path.join(HERE, "gates128_fdlibm.npz"), ops=g["ops"], a=g["a"], b=g["b"], out=out,
+             out_sha256=digest, params="128", sk_seed=42, ck_seed=43, twiddles="fdlibm")
+    print("gates128_fdlibm sha256", digest, "words differing from the glibc fixture:",
+          int((out != g["out"]).sum()), "of", out.size)
+
+
 def lut_uint4_vectors():
     """BASELINE config 5's bits: UINT4 keys from seeds (sk 42, ck 43), the LUT of
     f(x) = (x + 1) mod 16 (lut/generator.zig:85-135), every message 0..15 encrypted
@@ -157,6 +197,7 @@ def lut_uint4_vectors():
 
 
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["twiddles", "polymul_bigint", "oracle_vectors", "gates128_vectors", "lut_uint4_vectors"]
+    what = sys.argv[1:] or ["twiddles", "polymul_bigint", "oracle_vectors", "gates128_vectors",
+                            "gates128_fdlibm_vectors", "lut_uint4_vectors"]
     for name in what:
         globals()[name]()

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 1
+    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -48,6 +48,29 @@ def test_create_rejects_unsupported_params():
     h = C.c_void_p()
     assert lib.tfhe_gpu_create(C.byref(p), 0, C.byref(h)) == -1
     assert not h.value
+
+
+def test_create_multi_rejects_bad_arguments():
+    """tfhe_gpu_create_multi validates before touching a device (no GPU here)."""
+    lib = tfhe_amd.load_library()
+    p = tfhe_amd.make_params("128")
+    h = C.c_void_p()
+    assert lib.tfhe_gpu_create_multi(C.byref(p), 0, None, C.byref(h)) == -1
+    p.N = 512
+    assert lib.tfhe_gpu_create_multi(C.byref(p), 2, None, C.byref(h)) == -1
+    assert not h.value
+    assert lib.tfhe_gpu_num_devices(None) == 0
+
+
+def test_options_need_a_context():
+    lib = tfhe_amd.load_library()
+    v = C.c_int64()
+    assert lib.tfhe_gpu_set_option(None, tfhe_amd.OPTIONS["br_form"], 1) == -1
+    assert lib.tfhe_gpu_get_option(None, tfhe_amd.OPTIONS["br_form"], C.byref(v)) == -1
+    assert lib.tfhe_gpu_last_kernels(None) == b""
+    assert set(tfhe_amd.OPTIONS) == set(tfhe_amd.OPTION_DEFAULTS)
+    with pytest.raises(tfhe_amd.TfheError):
+        tfhe_amd.fft_tables(1000)
 
 
 @pytest.mark.parametrize("pname", ["128", "80", "uint4"])

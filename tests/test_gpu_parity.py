@@ -81,48 +81,50 @@ def test_external_product_vs_oracle(oracle, pname):
     assert np.array_equal(c.external_product(x, bk_index=5), want)
 
 
-@pytest.mark.parametrize("form", ["lanes", "sel"])
+@pytest.mark.parametrize("form", ["lanes", "lanes-narrow", "sel"])
 @pytest.mark.parametrize("pname,B", [("128", 9), ("128", 130), ("80", 1), ("80", 65), ("uint4", 17)])
-def test_key_switch_vs_oracle(oracle, pname, B, form, monkeypatch):
-    """Both key-switch forms (lane = item / lane = word) bit-exact, ragged B."""
-    monkeypatch.setenv("TFHE_KS_KERNEL", form)
+def test_key_switch_vs_oracle(oracle, pname, B, form):
+    """All key-switch forms (lane = item in wide / narrow blocks, lane = word) bit-exact, ragged B."""
     c, k = ctx_for(oracle, pname)
     lv1 = u32rand(rng(5), B, 1025)
     want = np.array([oracle.identity_key_switch(k.p, v, k.ck.ksk) for v in lv1])
-    assert np.array_equal(c.key_switch(lv1), want)
+    with c.options(ks_form=int(form == "sel"), ks_narrow=int(form.endswith("narrow"))):
+        assert np.array_equal(c.key_switch(lv1), want)
 
 
 # ---- blind rotation / bootstrap ---------------------------------------------
 @pytest.mark.parametrize("form", ["whole", "whole-noloader", "split", "wide"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
-def test_blind_rotate_vs_oracle(oracle, pname, B, form, monkeypatch):
+def test_blind_rotate_vs_oracle(oracle, pname, B, form):
     """All kernel forms (1 wave per item with or without loader waves / 2 waves
     per item / 8 waves per item) bit-exact."""
-    monkeypatch.setenv("TFHE_BR_KERNEL", form.split("-")[0])
-    monkeypatch.setenv("TFHE_BR_LOADER", "0" if form.endswith("noloader") else "1")
     c, k = ctx_for(oracle, pname)
     cts = u32rand(rng(6), B, k.p.n + 1)  # uniform TLWE: bit-exactness only
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
-    assert np.array_equal(c.blind_rotate_batch(cts), want)
     # odd batch sizes leave idle item slots in the last workgroup
     cts5 = u32rand(rng(16), 5, k.p.n + 1)
     want5 = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts5])
-    assert np.array_equal(c.blind_rotate_batch(cts5), want5)
+    with c.options(br_form=form.split("-")[0], br_loader=int(not form.endswith("noloader"))):
+        assert np.array_equal(c.blind_rotate_batch(cts), want)
+        assert c.last_kernels().startswith({"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<",
+                                            "wide": "k_blind_rotate_wide<"}[form.split("-")[0]])
+        assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
 @pytest.mark.parametrize("form", ["whole", "split", "wide"])
-def test_bootstrap_without_key_switch(oracle, form, monkeypatch):
+def test_bootstrap_without_key_switch(oracle, form):
     """VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69) and the
     strategy mirror: blind rotation + the hybrid sampleExtractIndex2."""
-    monkeypatch.setenv("TFHE_BR_KERNEL", form)
     c, k = ctx_for(oracle, "80")
     cts = u32rand(rng(26), 3, k.p.n + 1)
     want = np.array([oracle.bootstrap_without_key_switch(k.p, t, k.ck) for t in cts])
-    assert np.array_equal(c.bootstrap_without_key_switch_batch(cts), want)
-    bs = tfhe_amd.HipBootstrap(c)
-    assert np.array_equal(bs.bootstrap_without_key_switch(cts[0]), want[0])
-    assert np.array_equal(bs.bootstrap(cts[1]), oracle.bootstrap(k.p, cts[1], k.ck))
-    assert bs.name() == "mi355x"
+    want1 = oracle.bootstrap(k.p, cts[1], k.ck)
+    with c.options(br_form=form):
+        assert np.array_equal(c.bootstrap_without_key_switch_batch(cts), want)
+        bs = tfhe_amd.HipBootstrap(c)
+        assert np.array_equal(bs.bootstrap_without_key_switch(cts[0]), want[0])
+        assert np.array_equal(bs.bootstrap(cts[1]), want1)
+        assert bs.name() == "mi355x"
 
 
 def test_gate_golden_vectors(oracle):
@@ -184,13 +186,12 @@ def test_nand_batch_1024_128bit(oracle):
     assert np.array_equal(c.gate_batch(np.zeros(64, np.uint8), A[:64], B[:64]), out[:64])
 
 
-@pytest.mark.parametrize("loader", ["1", "0"])
-def test_gate_batch_rounds_and_tail(oracle, loader, monkeypatch):
+@pytest.mark.parametrize("loader", [1, 0])
+def test_gate_batch_rounds_and_tail(oracle, loader):
     """2,348 mixed gates (80-bit): two whole-form rounds of 1,024 plus a 300-gate tail
     that launch_blind_rotate hands to the latency form, on the plain (non-gathered)
     input path whose tail pointers it offsets.  Truth table for all, oracle bits at
     the round and tail boundaries, with and without loader waves."""
-    monkeypatch.setenv("TFHE_BR_LOADER", loader)
     c, k = ctx_for(oracle, "80")
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
     g = rng(31)
@@ -200,7 +201,8 @@ def test_gate_batch_rounds_and_tail(oracle, loader, monkeypatch):
     b_bits = g.integers(0, 2, n).astype(np.uint8)
     A = sk.encrypt_bool(a_bits, seed0=31_000)
     B = sk.encrypt_bool(b_bits, seed0=41_000)
-    out = c.gate_batch(ops, A, B)
+    with c.options(br_loader=loader):
+        out = c.gate_batch(ops, A, B)
     ab, bb = a_bits.astype(bool), b_bits.astype(bool)
     want_bits = np.zeros(n, bool)
     for o in range(10):  # TRUTH below works on numpy bool arrays
@@ -324,18 +326,18 @@ def test_device_resident_api_with_torch(oracle):
     assert np.array_equal(t_o.cpu().numpy().view(np.uint32), want)
 
 
-@pytest.mark.parametrize("gw", ["1", "2", "4", "8"])
-def test_lut_uint4_key_switch_item_groups(oracle, monkeypatch, gw):
-    """UINT4 key switch with 1, 2 or 4 item groups per block (TFHE_KS_GW; 4 is the
-    default above 64 items): 300 LUT bootstraps, outputs identical across forms,
+@pytest.mark.parametrize("gw", [1, 2, 4, 8])
+def test_lut_uint4_key_switch_item_groups(oracle, gw):
+    """UINT4 key switch with 1, 2, 4 or 8 item groups per block (TFHE_OPT_KS_ITEM_GROUPS;
+    4 is the default above 64 items): 300 LUT bootstraps, outputs identical across forms,
     samples past the first group bit-exact vs the oracle."""
     c, k = ctx_for(oracle, "uint4")
     tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (3 * x + 5) % 16)
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
     msgs = rng(23).integers(0, 16, 300).astype(np.uint32)
     cts = sk.encrypt_lwe_message(msgs, 16, seed0=4242)
-    monkeypatch.setenv("TFHE_KS_GW", gw)
-    out = c.bootstrap_lut_batch(cts, tv)
+    with c.options(ks_item_groups=gw):
+        out = c.bootstrap_lut_batch(cts, tv)
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (3 * msgs + 5) % 16)
     for i in (0, 63, 64, 200, 299):
         want = oracle.gate_batch(k.p, np.array([255], np.uint8), cts[i][None], cts[i][None], k.ck, testvec=tv)[0]
@@ -354,3 +356,63 @@ def test_gates128_golden_fixture():
     assert hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest() == str(g["out_sha256"])
     assert np.array_equal(out, g["out"])
     c.close()
+
+
+# ---- twiddle-table source (TFHE_OPT_TWIDDLES) ------------------
+def test_twiddle_source_uint4_matches_oracle_under_each_table(oracle):
+    """Where the libm choice matters (UINT4: Bg = 2^22, inexact external products),
+    the engine matches the oracle built with the same table, for both candidate
+    libms of a Zig build (glibc / fdlibm-musl), and the two tables give different
+    bits.  Keys from the oracle's keygen under each table (seeds 42/43)."""
+    p = get_keys(oracle, "uint4").p
+    tv = tfhe_amd.lut_generate(tfhe_amd.make_params("uint4"), 16, lambda x: (x + 1) % 16)
+    k0, k1 = oracle.secret_key(p, 42)
+    sk = tfhe_amd.SecretKey(tfhe_amd.make_params("uint4"), k0, k1)
+    msgs = np.arange(6, dtype=np.uint32) * 3 % 16
+    cts = sk.encrypt_lwe_message(msgs, 16, seed0=515)
+    outs = {}
+    for src in (0, 1):
+        try:
+            oracle.set_trig_source(src)
+            ck = oracle.cloud_key(p, 43, k0, k1)
+            want = oracle.gate_batch(p, np.full(msgs.size, 255, np.uint8), cts, cts, ck, testvec=tv, threads=6)
+        finally:
+            oracle.set_trig_source(0)
+        c = tfhe_amd.Context("uint4", 0)
+        c.set_option("twiddles", src)
+        assert c.get_option("twiddles") == src
+        c.load_cloud_key(ck.offset, ck.testvec, ck.bk, ck.ksk)
+        outs[src] = c.bootstrap_lut_batch(cts, tv)
+        c.close()
+        assert np.array_equal(outs[src], want)
+        assert np.array_equal(sk.decrypt_lwe_message(outs[src], 16), (msgs + 1) % 16)
+    assert (outs[0] != outs[1]).any()
+
+
+def test_gates128_fdlibm_golden_fixture():
+    """The 128-bit gate fixture regenerated under the fdlibm twiddles
+    (tests/golden/gates128_fdlibm.npz) from seeds on the GPU with TFHE_OPT_TWIDDLES =
+    fdlibm (keygen transforms the key with those tables)."""
+    import hashlib
+    g = np.load(os.path.join(GOLDEN, "gates128_fdlibm.npz"))
+    c = tfhe_amd.Context("128", 0)
+    c.set_option("twiddles", tfhe_amd.TWIDDLES_FDLIBM)
+    c.keygen(42, 43)
+    out = c.gate_batch(g["ops"], g["a"], g["b"])
+    assert hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest() == str(g["out_sha256"])
+    c.close()
+
+
+def test_options_validation_and_report(oracle):
+    """tfhe_gpu_set_option rejects unknown keys / values; the last-kernel report
+    names the default forms (loader-wave whole form + the wide lane key switch at 1,024
+    gates, the latency form below 512)."""
+    c, k = ctx_for(oracle, "128")
+    with pytest.raises(tfhe_amd.TfheError):
+        c.set_option("br_form", 9)
+    assert c.lib.tfhe_gpu_set_option(c.h, 99, 0) == -1
+    assert c.get_option("br_form") == 0
+    g = rng(91)
+    cts = u32rand(g, 3, k.p.n + 1)
+    c.bootstrap_batch(cts)
+    assert c.last_kernels() == "k_blind_rotate_wide<3,true> (latency form) + k_key_switch_lanes<9,2,32,4,1>"

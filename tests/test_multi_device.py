@@ -1,0 +1,127 @@
+"""Multi-device contexts (tfhe_gpu_create_multi): batches
+sharded over the devices in contiguous slices, the cloud key broadcast once
+(RCCL ncclBroadcast for distinct devices, a device-to-device copy for a device
+listed twice).  The GPU box has one MI355X, so the sharding is exercised with
+device 0 listed twice (two shards, two streams, two host threads) and the RCCL
+path with a one-device communicator; outputs must be bit-identical to a
+single-device context and to the oracle."""
+import numpy as np
+import pytest
+
+import tfhe_amd
+from conftest import get_keys, rng
+
+pytestmark = pytest.mark.gpu
+
+
+def u32rand(g, *shape):
+    return g.integers(0, 1 << 32, shape, dtype=np.uint64).astype(np.uint32)
+
+
+def loaded(oracle, pname, devices=None):
+    k = get_keys(oracle, pname)
+    c = tfhe_amd.Context(pname, 0) if devices is None else tfhe_amd.Context.multi(pname, devices=devices)
+    c.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    return c, k
+
+
+def test_rccl_broadcast_one_device(oracle):
+    """devices=[0]: ncclCommInitAll over one device + the in-place ncclBroadcast of the
+    BK/KSK; gates bit-exact vs the oracle."""
+    c, k = loaded(oracle, "80", devices=[0])
+    assert c.num_devices == 1
+    g = rng(71)
+    ops = np.arange(10, dtype=np.uint8)
+    A, B = u32rand(g, 10, k.p.n + 1), u32rand(g, 10, k.p.n + 1)
+    assert np.array_equal(c.gate_batch(ops, A, B), oracle.gate_batch(k.p, ops, A, B, k.ck, threads=8))
+    c.close()
+
+
+@pytest.mark.parametrize("B", [1, 37, 1100])
+def test_two_shards_gate_batch(oracle, B):
+    """Two shards on one GPU: ragged slices (1 item leaves the second shard idle,
+    1,100 = 550 + 550 runs the latency form on each), outputs in the caller's order."""
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0, 0])
+    assert multi.num_devices == 2
+    g = rng(72 + B)
+    ops = g.integers(0, 10, B).astype(np.uint8)
+    A, Bc = u32rand(g, B, k.p.n + 1), u32rand(g, B, k.p.n + 1)
+    want = single.gate_batch(ops, A, Bc)
+    assert np.array_equal(multi.gate_batch(ops, A, Bc), want)
+    idx = np.unique([0, B // 2, B - 1])
+    assert np.array_equal(want[idx], oracle.gate_batch(k.p, ops[idx], A[idx], Bc[idx], k.ck, threads=3))
+    single.close()
+    multi.close()
+
+
+def test_two_shards_every_batch_entry(oracle):
+    """bootstrap / bootstrap without key switch / blind rotation / key switch / LUT /
+    re-encryption through a two-shard context: identical to one device."""
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0, 0])
+    g = rng(73)
+    cts = u32rand(g, 9, k.p.n + 1)
+    assert np.array_equal(multi.bootstrap_batch(cts), single.bootstrap_batch(cts))
+    assert np.array_equal(multi.bootstrap_without_key_switch_batch(cts), single.bootstrap_without_key_switch_batch(cts))
+    assert np.array_equal(multi.blind_rotate_batch(cts[:5]), single.blind_rotate_batch(cts[:5]))
+    lv1 = u32rand(g, 7, 1025)
+    assert np.array_equal(multi.key_switch(lv1), single.key_switch(lv1))
+    tv = tfhe_amd.lut_generate(single.params, 4, lambda x: (x + 1) % 4)
+    assert np.array_equal(multi.bootstrap_lut_batch(cts, tv), single.bootstrap_lut_batch(cts, tv))
+    alice, bob = tfhe_amd.secret_key_new(single.params, 11), tfhe_amd.secret_key_new(single.params, 12)
+    key = tfhe_amd.ProxyReencryptionKey.new_symmetric(alice, bob, 1000)
+    bits = g.integers(0, 2, 13).astype(np.uint8)
+    enc = alice.encrypt_bool(bits, seed0=5)
+    r1, r2 = tfhe_amd.HipReencryptor(single, key), tfhe_amd.HipReencryptor(multi, key)
+    out = r2.reencrypt(enc)
+    assert np.array_equal(out, r1.reencrypt(enc))
+    assert np.array_equal(bob.decrypt_bool(out), bits.astype(bool))
+    r1.close()
+    r2.close()
+    # options reach every shard
+    with multi.options(br_form="whole"):
+        assert np.array_equal(multi.bootstrap_batch(cts), single.bootstrap_batch(cts))
+    single.close()
+    multi.close()
+
+
+def test_two_shards_keygen_broadcast(oracle):
+    """Keygen on the first device, D2D broadcast to the second: every shard's
+    result equals the oracle keygen's."""
+    p = get_keys(oracle, "80").p
+    multi = tfhe_amd.Context.multi("80", devices=[0, 0])
+    sk, _ = multi.keygen(42, 43)
+    k = get_keys(oracle, "80")
+    g = rng(74)
+    cts = u32rand(g, 4, p.n + 1)
+    want = np.array([oracle.bootstrap(p, t, k.ck) for t in cts])
+    assert np.array_equal(multi.bootstrap_batch(cts), want)  # items 2, 3 run on the second shard
+    multi.close()
+
+
+def test_two_shards_circuit_components(oracle):
+    """circuit_eval over two shards: two independent 16-bit adders (one component
+    each) land on different shards; 402 + 304 and 1234 + 4321, outputs identical to
+    one device, depth 33."""
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0, 0])
+    sk = tfhe_amd.SecretKey(single.params, k.k0, k.k1)
+    c = tfhe_amd.Circuit()
+    A = [[c.input() for _ in range(16)] for _ in range(2)]
+    Bw = [[c.input() for _ in range(16)] for _ in range(2)]
+    cin = [c.input() for _ in range(2)]
+    for j in range(2):
+        s, _ = c.ripple_add(A[j], Bw[j], cin[j])
+        c.output(*s)
+    xa, xb = [402, 1234], [304, 4321]
+    bits = [(xa[j] >> i) & 1 for j in range(2) for i in range(16)] + \
+           [(xb[j] >> i) & 1 for j in range(2) for i in range(16)] + [0, 0]
+    inputs = sk.encrypt_bool(bits, seed0=303)
+    got, depth = c.run(multi, inputs)
+    want, d1 = c.run(single, inputs)
+    assert depth == d1 == 33 and np.array_equal(got, want)
+    dec = sk.decrypt_bool(got).reshape(2, 16)
+    assert [sum(int(b) << i for i, b in enumerate(row)) for row in dec] == [706, 5555]
+    single.close()
+    multi.close()

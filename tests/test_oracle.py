@@ -6,6 +6,7 @@ oracle's semantics, and tests/golden/ pins independent exact values
 (big-int products, correctly rounded twiddles).
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -112,6 +113,86 @@ def test_twiddles_golden(oracle):
     d_re = np.abs(re.view(np.int64) - g["twist_re_cr"].view(np.int64))
     d_im = np.abs(im.view(np.int64) - g["twist_im_cr"].view(np.int64))
     assert d_re.max() <= 1 and d_im.max() <= 1
+
+
+def test_twiddles_fdlibm_golden(oracle):
+    """The second candidate libm (fdlibm/musl kernels, Zig compiler_rt): the oracle's
+    restatement, the product's (tfhe_fft_tables) and the Python one that made the
+    fixture (tests/golden/fdlibm_trig.py) agree bit for bit; so do the glibc tables.
+    The two sources differ in 43 twist entries and in no stage twiddle."""
+    import tfhe_amd
+    g = np.load(os.path.join(GOLDEN, "twiddles.npz"))
+    try:
+        oracle.set_trig_source(1)
+        re, im = oracle.twist_table(1024)
+        fr, fi = oracle.stage_twiddles(1024)
+    finally:
+        oracle.set_trig_source(0)
+    assert np.array_equal(re, g["twist_re_fdlibm"]) and np.array_equal(im, g["twist_im_fdlibm"])
+    assert np.array_equal(fr, g["stage_fwd_re_fdlibm"]) and np.array_equal(fi, g["stage_fwd_im_fdlibm"])
+    for src, sfx, st in ((0, "glibc", ""), (1, "fdlibm", "_fdlibm")):
+        tr, ti, sr, si = tfhe_amd.fft_tables(1024, src)
+        assert np.array_equal(tr, g["twist_re_" + sfx]) and np.array_equal(ti, g["twist_im_" + sfx])
+        assert np.array_equal(sr, g["stage_fwd_re" + st]) and np.array_equal(si, g["stage_fwd_im" + st])
+    n_twist = int((g["twist_re_glibc"] != g["twist_re_fdlibm"]).sum() + (g["twist_im_glibc"] != g["twist_im_fdlibm"]).sum())
+    assert n_twist == 43
+    assert np.array_equal(g["stage_fwd_re"], g["stage_fwd_re_fdlibm"])
+    # within 1 ulp of correct rounding, like glibc
+    assert np.abs(re.view(np.int64) - g["twist_re_cr"].view(np.int64)).max() <= 1
+    assert np.abs(im.view(np.int64) - g["twist_im_cr"].view(np.int64)).max() <= 1
+    sys.path.insert(0, GOLDEN)
+    import fdlibm_trig
+    assert all(fdlibm_trig.cos(float(i) * (np.pi / 1024)) == re[i] for i in range(512))
+
+
+def negacyclic_exact(a, b):
+    """a * b mod (X^N + 1) over the integers (int64 digits x u32 words), mod 2^32."""
+    N = a.size
+    c = np.convolve(a.astype(np.int64), b.astype(np.int64))
+    c = np.concatenate([c, [0]])
+    return ((c[:N] - c[N:]) % (1 << 32)).astype(np.uint32)
+
+
+@pytest.mark.parametrize("pname", ["128", "80"])
+def test_external_product_is_exact_integer(oracle, pname):
+    """At the L = 3 / Bg = 2^6 sets the f64 external product (trgsw.zig:111-154) rounds
+    to the EXACT integer result sum_i digit_i * row_i (negacyclic, mod 2^32) of the
+    TRGSW's integer rows: its float error stays far below 1/2.  So on these sets the
+    outputs do not depend on the FFT's rounding (nor on which libm made the
+    twiddles): checked here for random full-range rows under both twiddle sources."""
+    from oracle import params
+    p = params(pname)
+    g = rng(61)
+    off = oracle.decomposition_offset(p)
+    for src in (0, 1):
+        try:
+            oracle.set_trig_source(src)
+            for _ in range(3):
+                rows = g.integers(0, 1 << 32, (2 * p.L, 2, 1024), dtype=np.uint64).astype(np.uint32)
+                trgsw = np.array([[oracle.ifft(r[0]), oracle.ifft(r[1])] for r in rows])
+                x = g.integers(0, 1 << 32, 2048, dtype=np.uint64).astype(np.uint32)
+                got = oracle.external_product(p, trgsw, x, off)
+                dig = oracle.decomposition(p, x, off).view(np.int32)
+                want_a = np.zeros(1024, np.uint64)
+                want_b = np.zeros(1024, np.uint64)
+                for i in range(2 * p.L):
+                    want_a += negacyclic_exact(dig[i], rows[i][0])
+                    want_b += negacyclic_exact(dig[i], rows[i][1])
+                want = (np.concatenate([want_a, want_b]) % (1 << 32)).astype(np.uint32)
+                assert np.array_equal(got, want)
+        finally:
+            oracle.set_trig_source(0)
+
+
+def test_twiddle_source_changes_gates_only_where_inexact():
+    """Committed evidence (tests/golden/make_golden.py): the 128-bit gate fixture is
+    bit-identical under the glibc and the fdlibm twiddles (exact external products),
+    while the UINT4 set (Bg = 2^22: products past 2^53, inexact) is not; there the
+    engine takes the table source as a context option (TFHE_OPT_TWIDDLES)."""
+    a = np.load(os.path.join(GOLDEN, "gates128.npz"))
+    b = np.load(os.path.join(GOLDEN, "gates128_fdlibm.npz"))
+    assert np.array_equal(a["a"], b["a"]) and np.array_equal(a["out"], b["out"])
+    assert str(b["twiddles"]) == "fdlibm"
 
 
 # ---- trgsw.zig tests --------------------------------------------------------

@@ -1,10 +1,13 @@
+# rocprofv3 --pmc passes over br_only.py (one B=1024 NAND batch), one counter
+# group per pass (gfx950 block limits: <= 8 SQ, FETCH_SIZE alone, WRITE_SIZE alone).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${1:-pmc_br}
+B=${2:-1024}
 cd /tmp && export TMPDIR=/tmp
-rocprofv3 -L > $R/gpurun_out/counters_list.txt 2>&1 || true
 i=0
-for CTRS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_INT32" "SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64 SQ_INSTS_SMEM SQ_INSTS_BRANCH"; do
+for CTRS in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY"; do
   i=$((i+1))
-  timeout -k 10 180 rocprofv3 --pmc $CTRS --output-format csv -d $R/gpurun_out/$TAG/p$i -o run -- python $R/tools/br_only.py 1024 1 > $R/gpurun_out/${TAG}_p$i.log 2>&1 || echo "pass $i failed" >> $R/gpurun_out/${TAG}_fail.log
+  timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d $R/gpurun_out/$TAG/p$i -o run -- python3 $R/tools/br_only.py $B 1 > $R/gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i ($CTRS) failed"; exit 1; }
 done
+cd $R && python3 tools/pmc_traffic.py gpurun_out/$TAG $B 128 > gpurun_out/${TAG}_summary.json

@@ -1,0 +1,73 @@
+"""rocprofv3 --pmc passes over tools/br_only.py -> profiles/pmc_blind_rotate.json.
+
+Reads gpurun_out/<dir>/p*/run_counter_collection.csv (one counter group per
+pass, tools/pmc_br.sh), keeps the blind-rotation launches, and writes the
+per-launch figures bench.py reports as roofline.traffic / roofline.pmc,
+tagged with the kernel source hash so a later kernel change is not reported
+with these bytes.  FETCH_SIZE is doubled (MI355X_MICROARCH.md: gfx950 tallies
+128-B streaming requests at 64 B); counter KB -> bytes x 1024.
+
+    python tools/pmc_traffic.py gpurun_out/<dir> [batch] [params]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    d = sys.argv[1]
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    params = sys.argv[3] if len(sys.argv) > 3 else "128"
+    n = {"128": 700, "80": 550, "uint4": 820}[params]
+    tot = collections.defaultdict(float)
+    launches = collections.defaultdict(set)
+    name = None
+    for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            k = row["Kernel_Name"]
+            if "k_blind_rotate<" not in k:
+                continue
+            name = k.split("(")[0]
+            c = row["Counter_Name"]
+            tot[c] += float(row["Counter_Value"])
+            launches[c].add((f, row.get("Dispatch_Id", row.get("Correlation_Id", ""))))
+    if not tot:
+        raise SystemExit(f"no blind-rotation rows under {d}")
+    per = {c: tot[c] / max(1, len(launches[c])) for c in tot}
+    fetch = per.get("FETCH_SIZE", 0.0) * 1024 * 2
+    write = per.get("WRITE_SIZE", 0.0) * 1024
+    import bench  # noqa: E402  (kernel_source_hash)
+    rec = {
+        "kernel": name, "batch": batch, "params": params,
+        "kernel_source_sha256": bench.kernel_source_hash(),
+        "launches_per_pass": max(len(v) for v in launches.values()),
+        "hbm_bytes_per_launch": int(fetch + write) if "FETCH_SIZE" in per and "WRITE_SIZE" in per else None,
+        "fetch_bytes_corrected": int(fetch), "write_bytes": int(write),
+        "raw_per_launch": {c: per[c] for c in sorted(per)},
+        "method": ("rocprofv3 --pmc, one counter group per pass (tools/pmc_br.sh over tools/br_only.py "
+                   f"{batch} 1), blind-rotation dispatches only; FETCH_SIZE x2 (gfx950 rule), KB x1024"),
+    }
+    if "SQ_INSTS_VALU_ADD_F64" in per:
+        rec["valu_f64_insts_per_launch"] = per["SQ_INSTS_VALU_ADD_F64"] + per.get("SQ_INSTS_VALU_MUL_F64", 0.0)
+        rec["valu_fma_f64_insts_per_launch"] = per.get("SQ_INSTS_VALU_FMA_F64", 0.0)
+    if "SQ_INSTS_VALU" in per:  # gate waves = batch (the loader waves issue few VALU instructions)
+        rec["valu_insts_per_gate_wave_per_cmux"] = round(per["SQ_INSTS_VALU"] / batch / n, 1)
+    if "SQ_INSTS_LDS" in per:
+        rec["lds_insts_per_gate_wave_per_cmux"] = round(per["SQ_INSTS_LDS"] / batch / n, 1)
+    if "SQ_WAIT_ANY" in per and "SQ_WAVE_CYCLES" in per:
+        rec["wait_any_frac_all_waves"] = round(per["SQ_WAIT_ANY"] / per["SQ_WAVE_CYCLES"], 4)
+    if "SQ_ACTIVE_INST_VALU" in per and "SQ_WAVE_CYCLES" in per:
+        rec["valu_active_frac_all_waves"] = round(per["SQ_ACTIVE_INST_VALU"] / per["SQ_WAVE_CYCLES"], 4)
+    out = os.path.join(ROOT, "profiles", "pmc_blind_rotate.json")
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -3,12 +3,17 @@
 // all bootstrap arithmetic runs in tfhe_kernels.hip.
 #include "tfhe_gpu.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types and prototypes only: librccl is dlopen'ed on first multi-device key load
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "host_math.hpp"
@@ -46,6 +51,18 @@ struct tfhe_gpu_ctx {
     bool profiling = false;
     std::vector<hipEvent_t> events;
     size_t ev_used = 0;
+    // kernel-form options (tfhe_gpu_set_option) and what the last launch ran
+    LaunchOpts opts{};
+    int64_t circuit_pack = 1;
+    int64_t twiddle_source = TFHE_TWIDDLES_GLIBC;
+    const char *last_br = "", *last_ks = "";
+    std::string last_kernels;
+    // multi-device context (tfhe_gpu_create_multi): shards[0] is this context
+    // (device devices[0]); shards[k > 0] are owned single-device contexts.
+    // Empty for a single-device context.
+    std::vector<tfhe_gpu_ctx *> shards;
+    bool distinct_devices = true;    // RCCL needs each device once; else D2D copies
+    std::vector<ncclComm_t> comms;   // one communicator per shard, created on the first key broadcast
 };
 
 namespace {
@@ -166,9 +183,10 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
         HIPCHK(c, hipEventRecord(ev[0], c->stream));
     }
     HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, idx, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
-                                  lv1, out_mode, B, c->stream));
+                                  lv1, out_mode, B, c->stream, c->opts, &c->last_br));
     if (ev[1]) HIPCHK(c, hipEventRecord(ev[1], c->stream));
-    if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream));
+    c->last_ks = "";
+    if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream, c->opts, &c->last_ks));
     if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], c->stream));
     return TFHE_OK;
 }
@@ -243,6 +261,41 @@ void reenc_key_gen(uint32_t n, const uint32_t *key_from, uint32_t basebit, uint3
             }
 }
 
+int broadcast_key(tfhe_gpu_ctx *c);    // multi-device key broadcast (end of file)
+void destroy_shards(tfhe_gpu_ctx *c);  // sub-contexts and RCCL communicators (end of file)
+
+// FFT constant tables (fft.zig:92-106 twists, :590-616 recurrence) from the
+// chosen cos/sin source (host_math.hpp), uploaded to the context's device.
+int build_tables(tfhe_gpu_ctx *c, int source) {
+    std::vector<double> tre, tim, fre, fim, ire, iim;
+    host::twist_table(c->P.N, tre, tim, source);
+    host::stage_twiddles(c->P.N, false, fre, fim, source);
+    host::stage_twiddles(c->P.N, true, ire, iim, source);
+    // the inverse kernels use conj(forward): that must equal the inverse
+    // recurrence bit for bit (both sources have an odd sin and an even cos)
+    for (size_t i = 0; i < fre.size(); i++)
+        if (std::memcmp(&fre[i], &ire[i], 8) != 0 || -fim[i] != iim[i])
+            return fail(c, TFHE_ERR_INVALID, "inverse twiddle table is not the conjugate of the forward one");
+    std::vector<C2> tw2(tre.size()), st2(fre.size());
+    for (size_t i = 0; i < tre.size(); i++) tw2[i] = C2{tre[i], tim[i]};
+    for (size_t i = 0; i < fre.size(); i++) st2[i] = C2{fre[i], fim[i]};
+    // passA's bf_m1 (tfhe_kernels.hip) relies on W4[1].im == W8[2].im == -1.0 exactly
+    if (st2[2].y != -1.0 || st2[5].y != -1.0)
+        return fail(c, TFHE_ERR_INVALID, "twiddle table: W4[1] / W8[2] imaginary part is not exactly -1");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->d_twist) HIPCHK(c, hipMalloc((void **)&c->d_twist, sizeof(C2) * tw2.size()));
+    if (!c->d_tw) HIPCHK(c, hipMalloc((void **)&c->d_tw, sizeof(C2) * st2.size()));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // no launch may still read the old tables
+    HIPCHK(c, hipMemcpy(c->d_twist, tw2.data(), sizeof(C2) * tw2.size(), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_tw, st2.data(), sizeof(C2) * st2.size(), hipMemcpyHostToDevice));
+    c->twa[0] = st2[2];
+    c->twa[1] = st2[4];
+    c->twa[2] = st2[5];
+    c->twa[3] = st2[6];
+    c->twiddle_source = source;
+    return TFHE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -271,39 +324,7 @@ int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
         e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
         if (e != hipSuccess) { rc = hip_fail(c, e, "hipStreamCreate"); break; }
         c->stream = c->own_stream;
-        // FFT constant tables (fft.zig:92-106 twists, :590-616 recurrence)
-        std::vector<double> tre, tim, fre, fim, ire, iim;
-        host::twist_table(params->N, tre, tim);
-        host::stage_twiddles(params->N, false, fre, fim);
-        host::stage_twiddles(params->N, true, ire, iim);
-        // the inverse kernels use conj(forward): that must equal the
-        // inverse recurrence bit for bit (glibc sin is odd, cos even)
-        for (size_t i = 0; i < fre.size(); i++)
-            if (std::memcmp(&fre[i], &ire[i], 8) != 0 || -fim[i] != iim[i]) {
-                rc = fail(c, TFHE_ERR_INVALID, "inverse twiddle table is not the conjugate of the forward one");
-                break;
-            }
-        if (rc) break;
-        std::vector<C2> tw2(tre.size()), st2(fre.size());
-        for (size_t i = 0; i < tre.size(); i++) tw2[i] = C2{tre[i], tim[i]};
-        for (size_t i = 0; i < fre.size(); i++) st2[i] = C2{fre[i], fim[i]};
-        // passA's bf_m1 (tfhe_kernels.hip) relies on W4[1].im == W8[2].im == -1.0 exactly
-        if (st2[2].y != -1.0 || st2[5].y != -1.0) {
-            rc = fail(c, TFHE_ERR_INVALID, "twiddle table: W4[1] / W8[2] imaginary part is not exactly -1");
-            break;
-        }
-        c->twa[0] = st2[2];
-        c->twa[1] = st2[4];
-        c->twa[2] = st2[5];
-        c->twa[3] = st2[6];
-        if (hipMalloc((void **)&c->d_twist, sizeof(C2) * tw2.size()) != hipSuccess ||
-            hipMalloc((void **)&c->d_tw, sizeof(C2) * st2.size()) != hipSuccess) {
-            rc = fail(c, TFHE_ERR_OOM, "hipMalloc(tables)");
-            break;
-        }
-        e = hipMemcpy(c->d_twist, tw2.data(), sizeof(C2) * tw2.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(c->d_tw, st2.data(), sizeof(C2) * st2.size(), hipMemcpyHostToDevice);
-        if (e != hipSuccess) { rc = hip_fail(c, e, "upload tables"); break; }
+        rc = build_tables(c, TFHE_TWIDDLES_GLIBC);
     } while (0);
     if (rc != TFHE_OK) {
         std::fprintf(stderr, "tfhe_gpu_create: %s\n", c->err.c_str());
@@ -316,6 +337,7 @@ int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
 
 void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     if (!c) return;
+    destroy_shards(c);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
@@ -358,7 +380,7 @@ int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv
     HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));  // reference leaves k=0 rows undefined
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
-    return TFHE_OK;
+    return broadcast_key(c);
 }
 
 int tfhe_gpu_key_blob_bytes(const tfhe_gpu_ctx *c, size_t *bsk_bytes, size_t *ksk_bytes) {
@@ -392,7 +414,7 @@ int tfhe_gpu_import_key_device(tfhe_gpu_ctx *c, const void *bsk_dev, const void 
     HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
-    return TFHE_OK;
+    return broadcast_key(c);
 }
 
 // Device key -> reference host layout: BK un-permuted (and un-scaled) by
@@ -624,10 +646,10 @@ int tfhe_gpu_keygen(tfhe_gpu_ctx *c, uint64_t secret_seed, uint64_t cloud_seed, 
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (ksk_out) std::memcpy(ksk_out, ksk.data(), ksk.size() * sizeof(uint32_t));
     c->has_key = true;
-    return TFHE_OK;
+    return broadcast_key(c);
 }
 
-int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
+static int bootstrap_batch_one(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
     if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (B == 0) return TFHE_OK;
     HIPCHK(c, hipSetDevice(c->device));
@@ -639,7 +661,7 @@ int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out,
     return rc;
 }
 
-int tfhe_gpu_bootstrap_without_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
+static int bootstrap_without_key_switch_batch_one(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
     if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (B == 0) return TFHE_OK;
     HIPCHK(c, hipSetDevice(c->device));
@@ -651,7 +673,7 @@ int tfhe_gpu_bootstrap_without_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t 
     return rc;
 }
 
-int tfhe_gpu_gate_batch(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b, uint32_t *out,
+static int gate_batch_one(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b, uint32_t *out,
                         size_t B) {
     if (!c || (B && (!ops || !a || !b || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (B == 0) return TFHE_OK;
@@ -670,7 +692,7 @@ int tfhe_gpu_gate_batch(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, 
     return rc;
 }
 
-int tfhe_gpu_blind_rotate_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *trlwe_out,
+static int blind_rotate_batch_one(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *trlwe_out,
                                 size_t B) {
     if (!c || (B && (!in || !trlwe_out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (B == 0) return TFHE_OK;
@@ -688,7 +710,7 @@ int tfhe_gpu_blind_rotate_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint3
     return rc;
 }
 
-int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *out,
+static int bootstrap_lut_batch_one(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *out,
                                  size_t B) {
     if (!c || !testvec || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (B == 0) return TFHE_OK;
@@ -711,11 +733,12 @@ struct tfhe_gpu_reenc_key {
     int device = 0;
     uint32_t basebit = 0, t = 0;
     uint32_t *d_key = nullptr;  // padded rows like the KSK (K.ks_stride words) + zero tail
+    std::vector<tfhe_gpu_reenc_key *> peers;  // multi-device context: the copy on shard k is peers[k - 1]
 };
 
 extern "C" {
 
-int tfhe_gpu_reenc_key_load(tfhe_gpu_ctx *c, const uint32_t *key_encryptions, size_t len, uint32_t basebit,
+static int reenc_key_load_one(tfhe_gpu_ctx *c, const uint32_t *key_encryptions, size_t len, uint32_t basebit,
                             uint32_t t, tfhe_gpu_reenc_key **out) {
     if (!c || !key_encryptions || !out) return fail(c, TFHE_ERR_INVALID, "null argument");
     const size_t n = c->P.n, rows = n * t * ((size_t)1 << basebit);
@@ -750,12 +773,13 @@ int tfhe_gpu_reenc_key_load(tfhe_gpu_ctx *c, const uint32_t *key_encryptions, si
 
 void tfhe_gpu_reenc_key_destroy(tfhe_gpu_reenc_key *k) {
     if (!k) return;
+    for (tfhe_gpu_reenc_key *p : k->peers) tfhe_gpu_reenc_key_destroy(p);
     (void)hipSetDevice(k->device);
     (void)hipFree(k->d_key);
     delete k;
 }
 
-int tfhe_gpu_reencrypt_batch(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const uint32_t *in, uint32_t *out,
+static int reencrypt_batch_one(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const uint32_t *in, uint32_t *out,
                              size_t B) {
     if (!c || !k || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (k->device != c->device) return fail(c, TFHE_ERR_INVALID, "key belongs to another device");
@@ -766,7 +790,7 @@ int tfhe_gpu_reencrypt_batch(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
     if (rc) return rc;
     HIPCHK(c, launch_reencrypt(c->K, (int)k->t, (int)k->basebit, (const uint32_t *)c->s_a.p, k->d_key,
-                               (uint32_t *)c->s_out.p, B, c->stream));
+                               (uint32_t *)c->s_out.p, B, c->stream, c->opts, &c->last_ks));
     return d2h_sync(c, out, c->s_out.p, B * w * 4);
 }
 
@@ -820,7 +844,7 @@ int tfhe_reenc_key_gen_asymmetric(const tfhe_params *p, const uint32_t *key_from
 // 4 x #CUs gates, a ragged tail in the latency form).  Example: a level of
 // 10,256 gates hands 16 of them to the next level instead of running a
 // 16-gate tail.  Moved gates may move again from their new level.
-// TFHE_CIRCUIT_PACK=0 turns packing off (A/B runs and tests).
+// TFHE_OPT_CIRCUIT_PACK = 0 turns packing off (A/B runs and tests).
 static void pack_levels(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
                         const uint32_t *in_b, size_t cus, std::vector<uint32_t> &level,
                         std::vector<std::vector<uint32_t>> &bs) {
@@ -934,7 +958,7 @@ int tfhe_circuit_schedule(size_t n_inputs, size_t n_gates, const uint8_t *ops, c
 // evaluation order — inputs | NOTs of level 0 | gates of level 1 | NOTs of
 // level 1 | ... — so each level's batch writes one contiguous run of slots,
 // and its inputs are gathered by index inside the blind-rotation prologue.
-int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
+static int circuit_eval_one(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
                           const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
                           const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels_out) {
     if (!c || (n_inputs && !inputs) || (n_gates && (!ops || !in_a || !in_b)) || (n_outputs && (!out_wires || !outputs)))
@@ -945,9 +969,8 @@ int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inpu
     std::vector<uint32_t> ready;
     std::vector<std::vector<uint32_t>> bs, nots;
     uint32_t max_level = 0;
-    const char *pack_e = getenv("TFHE_CIRCUIT_PACK");
     HIPCHK(c, hipSetDevice(c->device));
-    if (const char *why = schedule_levels(n_inputs, n_gates, ops, in_a, in_b, !(pack_e && pack_e[0] == '0'),
+    if (const char *why = schedule_levels(n_inputs, n_gates, ops, in_a, in_b, c->circuit_pack != 0,
                                           device_cus(), ready, max_level, bs, nots))
         return fail(c, TFHE_ERR_INVALID, why);
     for (size_t o = 0; o < n_outputs; o++)
@@ -1121,7 +1144,7 @@ int tfhe_gpu_external_product_batch(tfhe_gpu_ctx *c, const double *trgsw_fft, ui
     return d2h_sync(c, out, c->s_out.p, B * 2048 * 4);
 }
 
-int tfhe_gpu_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t *in_lv1, uint32_t *out_lv0, size_t B) {
+static int key_switch_batch_one(tfhe_gpu_ctx *c, const uint32_t *in_lv1, uint32_t *out_lv0, size_t B) {
     if (!c || (B && (!in_lv1 || !out_lv0))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
     if (B == 0) return TFHE_OK;
@@ -1130,7 +1153,8 @@ int tfhe_gpu_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t *in_lv1, uint32_t 
     int rc = h2d(c, c->s_lv1, in_lv1, B * 1025 * 4);
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
     if (rc) return rc;
-    HIPCHK(c, launch_key_switch(c->K, (const uint32_t *)c->s_lv1.p, c->d_ksk, (uint32_t *)c->s_out.p, B, c->stream));
+    HIPCHK(c, launch_key_switch(c->K, (const uint32_t *)c->s_lv1.p, c->d_ksk, (uint32_t *)c->s_out.p, B, c->stream,
+                                c->opts, &c->last_ks));
     return d2h_sync(c, out_lv0, c->s_out.p, B * w * 4);
 }
 
@@ -1185,6 +1209,466 @@ int tfhe_lut_generate(const tfhe_params *p, uint32_t m, const uint32_t *f_table,
     for (size_t i = N - off; i < N; i++) tv[N + i] = ~tv[N + i] + 1u;
     for (size_t i = 0; i < N; i++) tv[i] = 0;
     return TFHE_OK;
+}
+
+}  // extern "C"
+
+// ---- Options ------------------------------------------------------------------
+extern "C" {
+
+int tfhe_gpu_set_option(tfhe_gpu_ctx *c, int key, int64_t v) {
+    if (!c) return TFHE_ERR_INVALID;
+    for (size_t d = 1; d < c->shards.size(); d++) {
+        int rc = tfhe_gpu_set_option(c->shards[d], key, v);
+        if (rc) return fail(c, rc, c->shards[d]->err);
+    }
+    LaunchOpts &o = c->opts;
+    switch (key) {
+    case TFHE_OPT_BR_FORM:
+        if (v < 0 || v > 3) break;
+        o.br_form = (int)v;
+        return TFHE_OK;
+    case TFHE_OPT_BR_LOADER:
+        if (v != 0 && v != 1) break;
+        o.br_loader = (int)v;
+        return TFHE_OK;
+    case TFHE_OPT_KS_FORM:
+        if (v != 0 && v != 1) break;
+        o.ks_form = (int)v;
+        return TFHE_OK;
+    case TFHE_OPT_KS_NARROW:
+        if (v != 0 && v != 1) break;
+        o.ks_narrow = (int)v;
+        return TFHE_OK;
+    case TFHE_OPT_KS_ITEM_GROUPS:
+        if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8) break;
+        o.ks_groups = (int)v;
+        return TFHE_OK;
+    case TFHE_OPT_KS_SEL_ITEMS:
+        if (v != 8 && v != 16 && v != 32) break;
+        o.ks_sel_items = (int)v;
+        return TFHE_OK;
+    case TFHE_OPT_CIRCUIT_PACK:
+        if (v != 0 && v != 1) break;
+        c->circuit_pack = v;
+        return TFHE_OK;
+    case TFHE_OPT_TWIDDLES:
+        if (v != TFHE_TWIDDLES_GLIBC && v != TFHE_TWIDDLES_FDLIBM) break;
+        return build_tables(c, (int)v);
+    default:
+        return fail(c, TFHE_ERR_INVALID, "unknown option key " + std::to_string(key));
+    }
+    return fail(c, TFHE_ERR_INVALID, "bad value " + std::to_string(v) + " for option " + std::to_string(key));
+}
+
+int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
+    if (!c || !v) return TFHE_ERR_INVALID;
+    const LaunchOpts &o = c->opts;
+    switch (key) {
+    case TFHE_OPT_BR_FORM: *v = o.br_form; break;
+    case TFHE_OPT_BR_LOADER: *v = o.br_loader; break;
+    case TFHE_OPT_KS_FORM: *v = o.ks_form; break;
+    case TFHE_OPT_KS_NARROW: *v = o.ks_narrow; break;
+    case TFHE_OPT_KS_ITEM_GROUPS: *v = o.ks_groups; break;
+    case TFHE_OPT_KS_SEL_ITEMS: *v = o.ks_sel_items; break;
+    case TFHE_OPT_CIRCUIT_PACK: *v = c->circuit_pack; break;
+    case TFHE_OPT_TWIDDLES: *v = c->twiddle_source; break;
+    default: return TFHE_ERR_INVALID;
+    }
+    return TFHE_OK;
+}
+
+const char *tfhe_gpu_last_kernels(tfhe_gpu_ctx *c) {
+    if (!c) return "";
+    c->last_kernels = c->last_br;
+    if (c->last_ks && c->last_ks[0]) c->last_kernels += std::string(" + ") + c->last_ks;
+    return c->last_kernels.c_str();
+}
+
+int tfhe_fft_tables(uint32_t N, int source, double *twist_re, double *twist_im, double *stage_re, double *stage_im) {
+    if (N < 4 || (N & (N - 1)) || (source != TFHE_TWIDDLES_GLIBC && source != TFHE_TWIDDLES_FDLIBM))
+        return TFHE_ERR_INVALID;
+    std::vector<double> a, b;
+    host::twist_table(N, a, b, source);
+    if (twist_re) std::memcpy(twist_re, a.data(), a.size() * 8);
+    if (twist_im) std::memcpy(twist_im, b.data(), b.size() * 8);
+    host::stage_twiddles(N, false, a, b, source);
+    if (stage_re) std::memcpy(stage_re, a.data(), a.size() * 8);
+    if (stage_im) std::memcpy(stage_im, b.data(), b.size() * 8);
+    return TFHE_OK;
+}
+
+}  // extern "C"
+
+// ---- Multi-device context ----------------------------------
+namespace {
+
+// librccl, loaded on the first multi-device key broadcast.  dlopen keeps the
+// library loadable where RCCL is absent and, under PyTorch, reuses the RCCL
+// that torch has already mapped (same SONAME) instead of a second copy.
+struct RcclApi {
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const RcclApi *rccl_api(std::string &why) {
+    static std::once_flag once;
+    static RcclApi api;
+    static std::string load_error;
+    std::call_once(once, [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+        if (!h) {
+            load_error = std::string("cannot load librccl.so.1: ") + dlerror();
+            return;
+        }
+        api.comm_init_all = (decltype(api.comm_init_all))dlsym(h, "ncclCommInitAll");
+        api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
+        api.broadcast = (decltype(api.broadcast))dlsym(h, "ncclBroadcast");
+        api.group_start = (decltype(api.group_start))dlsym(h, "ncclGroupStart");
+        api.group_end = (decltype(api.group_end))dlsym(h, "ncclGroupEnd");
+        api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+        if (!api.comm_init_all || !api.comm_destroy || !api.broadcast || !api.group_start || !api.group_end ||
+            !api.error_string)
+            load_error = "librccl.so.1 lacks an nccl* entry point";
+    });
+    why = load_error;
+    return load_error.empty() ? &api : nullptr;
+}
+
+bool is_multi(const tfhe_gpu_ctx *c) { return c && c->shards.size() > 1; }
+
+void destroy_shards(tfhe_gpu_ctx *c) {
+    if (!c->comms.empty()) {
+        std::string why;
+        if (const RcclApi *r = rccl_api(why))
+            for (ncclComm_t m : c->comms)
+                if (m) r->comm_destroy(m);
+        c->comms.clear();
+    }
+    for (size_t d = 1; d < c->shards.size(); d++) tfhe_gpu_destroy(c->shards[d]);
+    c->shards.clear();
+}
+
+// The key just loaded on shard 0 -> every other shard: one ncclBroadcast of
+// the device BK and KSK (RCCL over xGMI), or a device-to-device copy when a
+// device appears twice.  The test vector / offset are host state (8 KB).
+int broadcast_key(tfhe_gpu_ctx *c) {
+    if (c->shards.empty()) return TFHE_OK;
+    const size_t D = c->shards.size();
+    for (size_t d = 1; d < D; d++) {
+        tfhe_gpu_ctx *s = c->shards[d];
+        s->has_key = false;
+        HIPCHK(c, hipSetDevice(s->device));
+        int rc = set_key_common(s, c->offset, c->testvec.data(), c->testvec.data() + c->P.N);
+        if (rc) return fail(c, rc, s->err);
+        HIPCHK(c, hipStreamSynchronize(s->stream));
+    }
+    if (c->distinct_devices) {
+        std::string why;
+        const RcclApi *r = rccl_api(why);
+        if (!r) return fail(c, TFHE_ERR_HIP, why);
+        if (c->comms.empty()) {
+            std::vector<int> devs(D);
+            for (size_t d = 0; d < D; d++) devs[d] = c->shards[d]->device;
+            c->comms.assign(D, nullptr);
+            ncclResult_t e = r->comm_init_all(c->comms.data(), (int)D, devs.data());
+            if (e != ncclSuccess) {
+                c->comms.clear();
+                return fail(c, TFHE_ERR_HIP, std::string("ncclCommInitAll: ") + r->error_string(e));
+            }
+        }
+        ncclResult_t e = r->group_start();
+        for (size_t d = 0; d < D && e == ncclSuccess; d++) {
+            tfhe_gpu_ctx *s = c->shards[d];
+            e = r->broadcast(c->d_bk, s->d_bk, c->bk_bytes, ncclUint8, 0, c->comms[d], s->stream);
+            if (e == ncclSuccess) e = r->broadcast(c->d_ksk, s->d_ksk, c->ksk_bytes, ncclUint8, 0, c->comms[d], s->stream);
+        }
+        ncclResult_t e2 = r->group_end();
+        if (e == ncclSuccess) e = e2;
+        if (e != ncclSuccess) return fail(c, TFHE_ERR_HIP, std::string("ncclBroadcast: ") + r->error_string(e));
+    } else {
+        for (size_t d = 1; d < D; d++) {
+            tfhe_gpu_ctx *s = c->shards[d];
+            HIPCHK(c, hipSetDevice(s->device));
+            HIPCHK(c, hipMemcpyPeerAsync(s->d_bk, s->device, c->d_bk, c->device, c->bk_bytes, s->stream));
+            HIPCHK(c, hipMemcpyPeerAsync(s->d_ksk, s->device, c->d_ksk, c->device, c->ksk_bytes, s->stream));
+        }
+    }
+    for (size_t d = 1; d < D; d++) {
+        tfhe_gpu_ctx *s = c->shards[d];
+        HIPCHK(c, hipSetDevice(s->device));
+        HIPCHK(c, hipStreamSynchronize(s->stream));
+        s->has_key = true;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TFHE_OK;
+}
+
+// f(shard, first item, count) on every device's contiguous slice of B items
+// (ceil(B/D) each), concurrently: one host thread per device beyond the first.
+template <class F>
+int run_sharded(tfhe_gpu_ctx *c, size_t B, F f) {
+    const size_t D = c->shards.size(), per = (B + D - 1) / D;
+    std::vector<int> rc(D, TFHE_OK);
+    std::vector<std::thread> th;
+    for (size_t d = 1; d < D; d++) {
+        const size_t b0 = std::min(B, d * per), n = std::min(B, b0 + per) - b0;
+        if (n) th.emplace_back([&, d, b0, n] { rc[d] = f(c->shards[d], b0, n); });
+    }
+    if (B) rc[0] = f(c, 0, std::min(B, per));
+    for (std::thread &t : th) t.join();
+    for (size_t d = 1; d < D; d++)
+        if (rc[d]) return fail(c, rc[d], "device " + std::to_string(c->shards[d]->device) + ": " + c->shards[d]->err);
+    return rc[0];
+}
+
+struct Dsu {
+    std::vector<uint32_t> p;
+    explicit Dsu(size_t n) : p(n) { std::iota(p.begin(), p.end(), 0u); }
+    uint32_t find(uint32_t x) {
+        while (p[x] != x) x = p[x] = p[p[x]];
+        return x;
+    }
+    void unite(uint32_t a, uint32_t b) { p[find(a)] = find(b); }
+};
+
+// circuit_eval over the devices: the DAG's connected components (wires joined
+// by gates) go whole to one device each, largest first onto the least-loaded
+// device (bootstrapped gates), so each device evaluates an independent
+// sub-circuit with its own level schedule and no wire crosses devices.
+int circuit_eval_multi(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates, const uint8_t *ops,
+                       const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs, const uint32_t *out_wires,
+                       uint32_t *outputs, uint32_t *levels_out) {
+    const size_t W = n_inputs + n_gates, D = c->shards.size(), w1 = tlwe0_words(c);
+    {  // validate the whole graph first (same errors as one device)
+        std::vector<uint32_t> level;
+        std::vector<std::vector<uint32_t>> bs, nots;
+        uint32_t ml = 0;
+        if (const char *why = schedule_levels(n_inputs, n_gates, ops, in_a, in_b, false, 256, level, ml, bs, nots))
+            return fail(c, TFHE_ERR_INVALID, why);
+        for (size_t o = 0; o < n_outputs; o++)
+            if (out_wires[o] >= W) return fail(c, TFHE_ERR_INVALID, "output wire out of range");
+    }
+    Dsu dsu(W);
+    for (size_t g = 0; g < n_gates; g++) {
+        dsu.unite((uint32_t)(n_inputs + g), in_a[g]);
+        if (ops[g] <= TFHE_GATE_ORYN) dsu.unite((uint32_t)(n_inputs + g), in_b[g]);
+    }
+    std::vector<uint64_t> weight(W, 0);
+    for (size_t g = 0; g < n_gates; g++)
+        if (ops[g] != TFHE_GATE_NOT) weight[dsu.find((uint32_t)(n_inputs + g))]++;
+    std::vector<uint32_t> roots;
+    for (size_t w = 0; w < W; w++)
+        if (dsu.find((uint32_t)w) == w) roots.push_back((uint32_t)w);
+    std::stable_sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) { return weight[a] > weight[b]; });
+    std::vector<uint32_t> dev_of(W, 0);  // per component root
+    std::vector<uint64_t> load(D, 0);
+    for (uint32_t r : roots) {
+        const size_t d = std::min_element(load.begin(), load.end()) - load.begin();
+        dev_of[r] = (uint32_t)d;
+        load[d] += weight[r];
+    }
+    // per-device sub-circuits; wires renumbered: used inputs first, then gates
+    struct Sub {
+        std::vector<uint32_t> inputs, in_a, in_b, out_wires, out_index;
+        std::vector<uint8_t> ops;
+        std::vector<uint32_t> outputs;
+        uint32_t levels = 0;
+    };
+    std::vector<Sub> sub(D);
+    std::vector<uint32_t> local(W, 0xFFFFFFFFu);
+    auto dev = [&](uint32_t w) { return dev_of[dsu.find(w)]; };
+    auto use_input = [&](uint32_t w) {
+        if (w < n_inputs && local[w] == 0xFFFFFFFFu) {
+            Sub &s = sub[dev(w)];
+            local[w] = (uint32_t)s.inputs.size();
+            s.inputs.push_back(w);
+        }
+    };
+    for (size_t g = 0; g < n_gates; g++) {
+        use_input(in_a[g]);
+        if (ops[g] <= TFHE_GATE_ORYN) use_input(in_b[g]);
+    }
+    for (size_t o = 0; o < n_outputs; o++) use_input(out_wires[o]);
+    std::vector<uint32_t> gate_count(D, 0);
+    for (size_t g = 0; g < n_gates; g++) {
+        const uint32_t w = (uint32_t)(n_inputs + g), d = dev(w);
+        local[w] = gate_count[d]++;  // final id = #inputs of the device + this
+    }
+    auto id = [&](uint32_t w) { return w < n_inputs ? local[w] : (uint32_t)sub[dev(w)].inputs.size() + local[w]; };
+    for (size_t g = 0; g < n_gates; g++) {
+        Sub &s = sub[dev((uint32_t)(n_inputs + g))];
+        s.ops.push_back(ops[g]);
+        s.in_a.push_back(id(in_a[g]));
+        s.in_b.push_back(ops[g] <= TFHE_GATE_ORYN ? id(in_b[g]) : 0u);
+    }
+    for (size_t o = 0; o < n_outputs; o++) {
+        Sub &s = sub[dev(out_wires[o])];
+        s.out_wires.push_back(id(out_wires[o]));
+        s.out_index.push_back((uint32_t)o);
+    }
+    std::vector<int> rc(D, TFHE_OK);
+    auto run = [&](size_t d) {
+        Sub &s = sub[d];
+        if (s.ops.empty() && s.out_wires.empty()) return;
+        std::vector<uint32_t> in(s.inputs.size() * w1);
+        for (size_t i = 0; i < s.inputs.size(); i++)
+            std::memcpy(in.data() + i * w1, inputs + (size_t)s.inputs[i] * w1, w1 * 4);
+        s.outputs.resize(s.out_wires.size() * w1);
+        rc[d] = circuit_eval_one(c->shards[d], s.inputs.size(), in.data(), s.ops.size(), s.ops.data(), s.in_a.data(),
+                                 s.in_b.data(), s.out_wires.size(), s.out_wires.data(), s.outputs.data(), &s.levels);
+    };
+    std::vector<std::thread> th;
+    for (size_t d = 1; d < D; d++) th.emplace_back(run, d);
+    run(0);
+    for (std::thread &t : th) t.join();
+    uint32_t depth = 0;
+    for (size_t d = 0; d < D; d++) {
+        if (rc[d]) return fail(c, rc[d], "device " + std::to_string(c->shards[d]->device) + ": " + c->shards[d]->err);
+        const Sub &s = sub[d];
+        for (size_t k = 0; k < s.out_index.size(); k++)
+            std::memcpy(outputs + (size_t)s.out_index[k] * w1, s.outputs.data() + k * w1, w1 * 4);
+        depth = std::max(depth, s.levels);
+    }
+    if (levels_out) *levels_out = depth;
+    return TFHE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int *devices, tfhe_gpu_ctx **out) {
+    if (!out || num_devices < 1) return TFHE_ERR_INVALID;
+    *out = nullptr;
+    std::vector<int> devs(num_devices);
+    for (int d = 0; d < num_devices; d++) devs[d] = devices ? devices[d] : d;
+    tfhe_gpu_ctx *root = nullptr;
+    int rc = tfhe_gpu_create(params, devs[0], &root);
+    if (rc) return rc;
+    root->shards.push_back(root);
+    for (int d = 1; d < num_devices; d++) {
+        tfhe_gpu_ctx *s = nullptr;
+        rc = tfhe_gpu_create(params, devs[d], &s);
+        if (rc) {
+            tfhe_gpu_destroy(root);
+            return rc;
+        }
+        root->shards.push_back(s);
+    }
+    std::vector<int> sorted = devs;
+    std::sort(sorted.begin(), sorted.end());
+    root->distinct_devices = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    *out = root;
+    return TFHE_OK;
+}
+
+int tfhe_gpu_num_devices(const tfhe_gpu_ctx *c) { return !c ? 0 : c->shards.empty() ? 1 : (int)c->shards.size(); }
+
+int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
+    if (!is_multi(c)) return bootstrap_batch_one(c, in, out, B);
+    if (B && (!in || !out)) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t w = tlwe0_words(c);
+    return run_sharded(c, B, [&](tfhe_gpu_ctx *s, size_t b0, size_t n) {
+        return bootstrap_batch_one(s, in + b0 * w, out + b0 * w, n);
+    });
+}
+
+int tfhe_gpu_bootstrap_without_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
+    if (!is_multi(c)) return bootstrap_without_key_switch_batch_one(c, in, out, B);
+    if (B && (!in || !out)) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t w = tlwe0_words(c);
+    return run_sharded(c, B, [&](tfhe_gpu_ctx *s, size_t b0, size_t n) {
+        return bootstrap_without_key_switch_batch_one(s, in + b0 * w, out + b0 * w, n);
+    });
+}
+
+int tfhe_gpu_gate_batch(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b, uint32_t *out,
+                        size_t B) {
+    if (!is_multi(c)) return gate_batch_one(c, ops, a, b, out, B);
+    if (B && (!ops || !a || !b || !out)) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t w = tlwe0_words(c);
+    return run_sharded(c, B, [&](tfhe_gpu_ctx *s, size_t b0, size_t n) {
+        return gate_batch_one(s, ops + b0, a + b0 * w, b + b0 * w, out + b0 * w, n);
+    });
+}
+
+int tfhe_gpu_blind_rotate_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *trlwe_out,
+                                size_t B) {
+    if (!is_multi(c)) return blind_rotate_batch_one(c, in, testvec, trlwe_out, B);
+    if (B && (!in || !trlwe_out)) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t w = tlwe0_words(c), wo = 2 * (size_t)c->P.N;
+    return run_sharded(c, B, [&](tfhe_gpu_ctx *s, size_t b0, size_t n) {
+        return blind_rotate_batch_one(s, in + b0 * w, testvec, trlwe_out + b0 * wo, n);
+    });
+}
+
+int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *c, const uint32_t *in, const uint32_t *testvec, uint32_t *out,
+                                 size_t B) {
+    if (!is_multi(c)) return bootstrap_lut_batch_one(c, in, testvec, out, B);
+    if (!testvec || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t w = tlwe0_words(c);
+    return run_sharded(c, B, [&](tfhe_gpu_ctx *s, size_t b0, size_t n) {
+        return bootstrap_lut_batch_one(s, in + b0 * w, testvec, out + b0 * w, n);
+    });
+}
+
+int tfhe_gpu_key_switch_batch(tfhe_gpu_ctx *c, const uint32_t *in_lv1, uint32_t *out_lv0, size_t B) {
+    if (!is_multi(c)) return key_switch_batch_one(c, in_lv1, out_lv0, B);
+    if (B && (!in_lv1 || !out_lv0)) return fail(c, TFHE_ERR_INVALID, "null argument");
+    const size_t w = tlwe0_words(c), wi = (size_t)c->P.N + 1;
+    return run_sharded(c, B, [&](tfhe_gpu_ctx *s, size_t b0, size_t n) {
+        return key_switch_batch_one(s, in_lv1 + b0 * wi, out_lv0 + b0 * w, n);
+    });
+}
+
+int tfhe_gpu_reenc_key_load(tfhe_gpu_ctx *c, const uint32_t *key_encryptions, size_t len, uint32_t basebit,
+                            uint32_t t, tfhe_gpu_reenc_key **out) {
+    int rc = reenc_key_load_one(c, key_encryptions, len, basebit, t, out);
+    if (rc || !is_multi(c)) return rc;
+    for (size_t d = 1; d < c->shards.size(); d++) {  // one upload per device (host -> each HBM)
+        tfhe_gpu_reenc_key *k = nullptr;
+        rc = reenc_key_load_one(c->shards[d], key_encryptions, len, basebit, t, &k);
+        if (rc) {
+            tfhe_gpu_reenc_key_destroy(*out);
+            *out = nullptr;
+            return fail(c, rc, c->shards[d]->err);
+        }
+        (*out)->peers.push_back(k);
+    }
+    return TFHE_OK;
+}
+
+int tfhe_gpu_reencrypt_batch(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const uint32_t *in, uint32_t *out,
+                             size_t B) {
+    if (!is_multi(c)) return reencrypt_batch_one(c, k, in, out, B);
+    if (!k || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (k->peers.size() + 1 != c->shards.size()) return fail(c, TFHE_ERR_INVALID, "key was not loaded on this context");
+    const size_t w = tlwe0_words(c);
+    return run_sharded(c, B, [&](tfhe_gpu_ctx *s, size_t b0, size_t n) {
+        size_t d = 0;
+        while (c->shards[d] != s) d++;
+        return reencrypt_batch_one(s, d ? k->peers[d - 1] : k, in + b0 * w, out + b0 * w, n);
+    });
+}
+
+int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates, const uint8_t *ops,
+                          const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs, const uint32_t *out_wires,
+                          uint32_t *outputs, uint32_t *levels) {
+    if (!is_multi(c))
+        return circuit_eval_one(c, n_inputs, inputs, n_gates, ops, in_a, in_b, n_outputs, out_wires, outputs, levels);
+    if ((n_inputs && !inputs) || (n_gates && (!ops || !in_a || !in_b)) || (n_outputs && (!out_wires || !outputs)))
+        return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    if (n_inputs + n_gates > 0xFFFFFFFFull) return fail(c, TFHE_ERR_INVALID, "too many wires");
+    return circuit_eval_multi(c, n_inputs, inputs, n_gates, ops, in_a, in_b, n_outputs, out_wires, outputs, levels);
 }
 
 }  // extern "C"

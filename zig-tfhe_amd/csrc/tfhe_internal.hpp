@@ -47,12 +47,26 @@ struct DevTables {
     C2 twa[4];        // tw[2], tw[4], tw[5], tw[6]: the lane-uniform pass-A twiddles, by value (SGPRs)
 };
 
+// Kernel-form choices of one context (tfhe_gpu_set_option, include/tfhe_gpu.h
+// TFHE_OPT_*).  The defaults are the measured-fastest forms; the others stay
+// for A/B runs and parity tests.  `used` (may be NULL) receives the name of
+// the kernel a launcher ran.
+struct LaunchOpts {
+    int br_form = 0;     // 0 auto, 1 whole, 2 split, 3 latency (wide)
+    int br_loader = 1;   // whole form: 1 loader waves issue the BK DMAs, 0 the gate waves do
+    int ks_form = 0;     // 0 lanes, 1 select / gather
+    int ks_narrow = 0;   // basebit 2: 1 forces the 32-word x 4-wave blocks
+    int ks_groups = 0;   // basebit >= 5: item groups per block (0 auto = 4; 1, 2, 4, 8)
+    int ks_sel_items = 8;  // select/gather form: items per block (8, 16, 32)
+};
+
 // ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------
 // idx: NULL, or B pairs (a, b) of ciphertext indices into in_a / in_b (circuit gather)
 hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out,
-                               int out_mode, size_t B, hipStream_t s);
+                               int out_mode, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),
+                               const char **used = nullptr);
 // CUs of the current device (256 when it cannot be queried) and
 // launch_blind_rotate's modelled time for B items on `cus` CUs, in whole-form
 // rounds of 4 x cus items (the circuit scheduler's level packing)
@@ -63,7 +77,8 @@ double blind_rotate_cost(size_t B, size_t cus);
 hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint32_t *idx, uint32_t *dst,
                               size_t count, bool negate, hipStream_t s);
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
-                             uint32_t *out, size_t B, hipStream_t s);
+                             uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),
+                             const char **used = nullptr);
 // zero the k = 0 rows (never read by the reference; the kernels subtract them unconditionally)
 hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s);
 // same for a key-switch-shaped key over n_in input coefficients (proxy re-encryption key)
@@ -71,9 +86,9 @@ hipError_t launch_key_zero_k0(const KParams &P, uint32_t *key, int n_in, int t, 
 // reencryptTLWELv0 (proxy_reenc.zig:267-306): key-switch-shaped key of n*t*2^basebit
 // rows in the padded device layout; in/out B TLWELv0
 hipError_t launch_reencrypt(const KParams &P, int t, int basebit, const uint32_t *in, const uint32_t *key,
-                            uint32_t *out, size_t B, hipStream_t s);
+                            uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),
+                            const char **used = nullptr);
 bool reencrypt_supported(int t, int basebit);
-// key-switch kernel form: 0 = lanes (default), 1 = select/gather (development knob TFHE_KS_KERNEL)
 hipError_t launch_fft_forward(const DevTables &T, const uint32_t *in, double *out, size_t B,
                               hipStream_t s);
 hipError_t launch_fft_inverse(const DevTables &T, const double *in, uint32_t *out, size_t B,

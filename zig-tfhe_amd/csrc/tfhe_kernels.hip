@@ -1636,21 +1636,17 @@ hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint3
 static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
-                               hipStream_t s, char forced) {
+                               hipStream_t s, char form, const LaunchOpts &O, const char **used) {
     if (B == 0) return hipSuccess;
     const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
     // |external product| <= 2L * N * Bg/2 * 2^31: the 8-op exact conversion
     // needs it below 2^51 (true for the L=3 / Bg=2^6 sets, false for UINT4)
     const bool small = std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 50);
-    // kernel form: wide (8 waves per item) for batches up to BR_WIDE_MAX_ITEMS,
-    // else whole (1 wave per item); split (2 waves per item) on request.
-    // Knob TFHE_BR_KERNEL=whole|split|wide forces a form (A/B runs and tests).
-    const bool split = forced == 's';
-    // latency form for batches below one gate per SIMD pair
-    const bool wide = forced ? forced == 'W' : B <= BR_WIDE_MAX_ITEMS;
-    // whole form: with loader waves unless TFHE_BR_LOADER=0 (A/B runs and tests)
-    const char *loader_e = getenv("TFHE_BR_LOADER");
-    const bool loader = !wide && !split && !(loader_e && loader_e[0] == '0');
+    // form: 'W' latency (8 waves per item), 's' split (2 waves per item),
+    // 'w' whole (1 wave per item; loader waves unless LaunchOpts::br_loader = 0)
+    const bool split = form == 's';
+    const bool wide = form == 'W';
+    const bool loader = !wide && !split && O.br_loader != 0;
     dim3 grid, block;
     if (wide) {
         grid = dim3((unsigned)B);
@@ -1664,18 +1660,23 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     }
 #define BR_LAUNCH(L_, S_)                                                                                         \
     do {                                                                                                          \
-        if (wide)                                                                                                 \
+        if (wide) {                                                                                               \
             hipLaunchKernelGGL((k_blind_rotate_wide<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,      \
                                testvec, bk2, out, out_mode, B);                                                   \
-        else if (split)                                                                                           \
+            if (used) *used = "k_blind_rotate_wide<" #L_ "," #S_ "> (latency form)";                              \
+        } else if (split) {                                                                                       \
             hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
                                testvec, bk2, out, out_mode, B);                                                   \
-        else if (loader)                                                                                          \
+            if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ "> (split form)";                               \
+        } else if (loader) {                                                                                      \
             hipLaunchKernelGGL((k_blind_rotate<L_, S_, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
                                testvec, bk2, out, out_mode, B);                                                   \
-        else                                                                                                      \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true> (whole form, loader waves)";                  \
+        } else {                                                                                                  \
             hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,  \
                                bk2, out, out_mode, B);                                                            \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",false> (whole form)";                               \
+        }                                                                                                         \
     } while (0)
     switch (P.L) {
     case 1: if (small) BR_LAUNCH(1, true); else BR_LAUNCH(1, false); break;
@@ -1687,8 +1688,8 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     return hipGetLastError();
 }
 
-// Kernel form per batch.  TFHE_BR_KERNEL=whole|split|wide forces one form for
-// the whole batch (A/B runs and tests).  Otherwise: the latency form up to
+// Kernel form per batch.  LaunchOpts::br_form (TFHE_OPT_BR_FORM) forces one
+// form for the whole batch (A/B runs and tests).  Otherwise: the latency form up to
 // BR_WIDE_MAX_ITEMS; above it the whole form, except that a ragged last round
 // of at most BR_TAIL_WIDE_MAX items (the whole form runs 4 items x #CUs per
 // round) goes to the latency form, which takes ~4.2 ms for up to 256 items and
@@ -1723,32 +1724,33 @@ double blind_rotate_cost(size_t B, size_t cus) {
 hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
-                               hipStream_t s) {
+                               hipStream_t s, const LaunchOpts &O, const char **used) {
     if (B == 0) return hipSuccess;
-    const char *form = getenv("TFHE_BR_KERNEL");
-    if (form) {
-        const char f = form[0] == 's' ? 's' : (form[0] == 'W' || (form[0] == 'w' && form[1] == 'i')) ? 'W' : 'w';
-        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f);
+    if (O.br_form) {  // forced form (TFHE_OPT_BR_FORM): the whole batch in one launch
+        const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : 'w';
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
-    if (B <= BR_WIDE_MAX_ITEMS) return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 0);
+    if (B <= BR_WIDE_MAX_ITEMS)
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'W', O, used);
     const size_t round = BR_WAVES * device_cus(), tail = B % round;
     if (tail == 0 || tail > BR_TAIL_WIDE_MAX || B < round)
-        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'w');
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'w', O, used);
     const size_t main = B - tail;
-    hipError_t e = launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, main, s, 'w');
+    hipError_t e = launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, main, s, 'w', O, used);
     if (e != hipSuccess) return e;
     // the tail: items main..B-1 (their ops / idx entries / inputs / outputs)
     const size_t in_words = (size_t)P.n + 1;
     const size_t out_words = out_mode == BR_OUT_LV1 ? (size_t)P.N + 1 : out_mode == BR_OUT_TRLWE ? 2 * (size_t)P.N : in_words;
     return launch_blind_rotate_form(P, T, ops ? ops + main : nullptr, idx ? in_a : in_a + main * in_words,
                                     idx ? in_b : (in_b ? in_b + main * in_words : nullptr), idx ? idx + 2 * main : nullptr,
-                                    testvec, bkd, out + main * out_words, out_mode, tail, s, 'W');
+                                    testvec, bkd, out + main * out_words, out_mode, tail, s, 'W', O, nullptr);
 }
 
 // lane-form key switch over an input of n_in coefficients (+ b); false if
 // (t, basebit) has no instantiation
 static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_t *in, int n_in, int in_stride,
-                            const uint32_t *key, uint32_t *out, size_t B, hipStream_t s) {
+                            const uint32_t *key, uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O,
+                            const char **used) {
     const unsigned groups = (unsigned)((B + 63) / 64);
     dim3 grid((unsigned)((P.ks_stride + KL_CHUNK - 1) / KL_CHUNK), groups), block(64 * KL_WAVES);
     // basebit 2 (128/80-bit): the 44-word x 8-wave blocks when they spread the
@@ -1756,12 +1758,15 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
     // block); 1024 gates at 128-bit: 1 round x 11 pieces instead of 2 x 8
     const unsigned wide_chunks = (unsigned)((P.ks_stride + KL_CHUNK_WIDE - 1) / KL_CHUNK_WIDE);
     const size_t rounds = (grid.x * (size_t)groups + 255) / 256, rounds_w = (wide_chunks * (size_t)groups + 255) / 256;
-    const bool wide = basebit == 2 && !getenv("TFHE_KS_NARROW") && rounds_w * (KL_CHUNK_WIDE / 4) < rounds * (KL_CHUNK / 4);
+    const bool wide = basebit == 2 && !O.ks_narrow && rounds_w * (KL_CHUNK_WIDE / 4) < rounds * (KL_CHUNK / 4);
     if (wide) {
         dim3 gw(wide_chunks, groups), bw(64 * KL_WAVES_WIDE);
 #define KS_WIDE(T_)                                                                                                     \
-    hipLaunchKernelGGL((k_key_switch_lanes<T_, 2, KL_CHUNK_WIDE, KL_WAVES_WIDE>), gw, bw, 0, s, P, in, key, out, B, \
-                       n_in, in_stride)
+    do {                                                                                                                \
+        hipLaunchKernelGGL((k_key_switch_lanes<T_, 2, KL_CHUNK_WIDE, KL_WAVES_WIDE>), gw, bw, 0, s, P, in, key, out, B, \
+                           n_in, in_stride);                                                                            \
+        if (used) *used = "k_key_switch_lanes<" #T_ ",2,44,8,1>";                                                       \
+    } while (0)
         if (t_ == 9) KS_WIDE(9);
         else if (t_ == 8) KS_WIDE(8);
         else if (t_ == 7) KS_WIDE(7);
@@ -1770,13 +1775,12 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
         return true;
     }
     // UINT4 (basebit 5): the 323 MB KSK streams from HBM once per item group, so
-    // 4 groups per block share each chunk through L2 (TFHE_KS_GW=1 forces one)
-    const char *gw_e = getenv("TFHE_KS_GW");
-    const int gw_env = gw_e ? atoi(gw_e) : 0;
-    const int gw = gw_env ? gw_env : (basebit >= 5 ? 4 : 1);
+    // 4 groups per block share each chunk through L2 (LaunchOpts::ks_groups forces 1, 2, 4 or 8)
+    const int gw = O.ks_groups ? O.ks_groups : (basebit >= 5 ? 4 : 1);
     if (gw == 8 && basebit == 5 && t_ == 3 && B > 64) {  // 16-word chunks: 8 rings fit the LDS
         dim3 g8((unsigned)((P.ks_stride + 15) / 16), (unsigned)((B + 511) / 512)), b8(512);
         hipLaunchKernelGGL((k_key_switch_lanes<3, 5, 16, 8, 8>), g8, b8, 0, s, P, in, key, out, B, n_in, in_stride);
+        if (used) *used = "k_key_switch_lanes<3,5,16,8,8>";
         return true;
     }
     if (gw == 4 && basebit == 5 && B > 64) {
@@ -1784,6 +1788,7 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
         if (t_ == 3) hipLaunchKernelGGL((k_key_switch_lanes<3, 5, KL_CHUNK, 4, 4>), g4, b4, 0, s, P, in, key, out, B, n_in, in_stride);
         else if (t_ == 2) hipLaunchKernelGGL((k_key_switch_lanes<2, 5, KL_CHUNK, 4, 4>), g4, b4, 0, s, P, in, key, out, B, n_in, in_stride);
         else return false;
+        if (used) *used = t_ == 3 ? "k_key_switch_lanes<3,5,32,4,4>" : "k_key_switch_lanes<2,5,32,4,4>";
         return true;
     }
     if (gw == 2 && basebit == 5 && B > 64) {
@@ -1791,10 +1796,14 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
         if (t_ == 3) hipLaunchKernelGGL((k_key_switch_lanes<3, 5, KL_CHUNK, 4, 2>), g2, b2, 0, s, P, in, key, out, B, n_in, in_stride);
         else if (t_ == 2) hipLaunchKernelGGL((k_key_switch_lanes<2, 5, KL_CHUNK, 4, 2>), g2, b2, 0, s, P, in, key, out, B, n_in, in_stride);
         else return false;
+        if (used) *used = t_ == 3 ? "k_key_switch_lanes<3,5,32,4,2>" : "k_key_switch_lanes<2,5,32,4,2>";
         return true;
     }
-#define KS_LANES(T_, BB_)                                                                                 \
-    hipLaunchKernelGGL((k_key_switch_lanes<T_, BB_>), grid, block, 0, s, P, in, key, out, B, n_in, in_stride)
+#define KS_LANES(T_, BB_)                                                                                     \
+    do {                                                                                                      \
+        hipLaunchKernelGGL((k_key_switch_lanes<T_, BB_>), grid, block, 0, s, P, in, key, out, B, n_in, in_stride); \
+        if (used) *used = "k_key_switch_lanes<" #T_ "," #BB_ ",32,4,1>";                                      \
+    } while (0)
     if (basebit == 2 && t_ == 9) KS_LANES(9, 2);
     else if (basebit == 2 && t_ == 8) KS_LANES(8, 2);
     else if (basebit == 2 && t_ == 7) KS_LANES(7, 2);
@@ -1809,9 +1818,9 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
 }
 
 hipError_t launch_reencrypt(const KParams &P, int t_, int basebit, const uint32_t *in, const uint32_t *key,
-                            uint32_t *out, size_t B, hipStream_t s) {
+                            uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (B == 0) return hipSuccess;
-    if (!launch_ks_lanes(P, t_, basebit, in, P.n, P.n + 1, key, out, B, s)) return hipErrorInvalidValue;
+    if (!launch_ks_lanes(P, t_, basebit, in, P.n, P.n + 1, key, out, B, s, O, used)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
@@ -1821,18 +1830,14 @@ bool reencrypt_supported(int t_, int basebit) {
 }
 
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk, uint32_t *out,
-                             size_t B, hipStream_t s) {
+                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (B == 0) return hipSuccess;
-    // kernel form: lanes (default) or the select/gather forms (TFHE_KS_KERNEL=sel, A/B and tests)
-    const char *form = getenv("TFHE_KS_KERNEL");
-    if (!(form && form[0] == 's') && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s))
+    // kernel form: lanes (default) or the select/gather forms (TFHE_OPT_KS_FORM = 1)
+    if (O.ks_form == 0 && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s, O, used))
         return hipGetLastError();
-    // items per block: development knob TFHE_KS_G in {8, 16, 32} (default 8)
-    static const int G = [] {
-        const char *e = getenv("TFHE_KS_G");
-        int v = e ? atoi(e) : 8;
-        return (v == 16 || v == 32) ? v : 8;
-    }();
+    // items per block: TFHE_OPT_KS_SEL_ITEMS in {8, 16, 32} (default 8)
+    const int G = (O.ks_sel_items == 16 || O.ks_sel_items == 32) ? O.ks_sel_items : 8;
+    if (used) *used = P.basebit == 2 ? "k_key_switch_sel" : "k_key_switch_gather";
     dim3 grid((unsigned)((P.n + 1 + 255) / 256), (unsigned)((B + G - 1) / G)), block(256);
 #define KS_SEL(T_, G_) hipLaunchKernelGGL((k_key_switch_sel<T_, G_>), grid, block, 0, s, P, lv1, ksk, out, B)
 #define KS_GATHER(T_, G_) hipLaunchKernelGGL((k_key_switch_gather<T_, G_>), grid, block, 0, s, P, lv1, ksk, out, B)

@@ -11,6 +11,7 @@ TLWELv0 values laid out exactly as `TLWELv0.p` (tlwe.zig:11-12).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 from dataclasses import dataclass
@@ -19,6 +20,14 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TFHE_GPU_LIB") or os.path.join(HERE, "lib", "libtfhe_gpu.so")  # env: A/B builds
+
+# tfhe_gpu_set_option keys / values (include/tfhe_gpu.h TFHE_OPT_*, TFHE_TWIDDLES_*)
+OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_groups": 5, "ks_sel_items": 6,
+           "circuit_pack": 7, "twiddles": 8}
+OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 0, "ks_narrow": 0, "ks_item_groups": 0,
+                   "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0}
+BR_FORMS = {"auto": 0, "whole": 1, "split": 2, "wide": 3}
+TWIDDLES_GLIBC, TWIDDLES_FDLIBM = 0, 1
 
 # gate op codes, include/tfhe_gpu.h TFHE_GATE_* (gates.zig:48-121)
 NAND, OR, AND, XOR, XNOR, NOR, ANDNY, ANDYN, ORNY, ORYN = range(10)
@@ -72,6 +81,12 @@ _SIGS = {
     "tfhe_gpu_last_error": (C.c_char_p, [vp]),
     "tfhe_gpu_sync": (C.c_int, [vp]),
     "tfhe_gpu_set_stream": (C.c_int, [vp, vp]),
+    "tfhe_gpu_create_multi": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
+    "tfhe_gpu_num_devices": (C.c_int, [vp]),
+    "tfhe_gpu_set_option": (C.c_int, [vp, C.c_int, C.c_int64]),
+    "tfhe_gpu_get_option": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int64)]),
+    "tfhe_gpu_last_kernels": (C.c_char_p, [vp]),
+    "tfhe_fft_tables": (C.c_int, [C.c_uint32, C.c_int, f64p, f64p, f64p, f64p]),
     "tfhe_gpu_load_cloud_key": (C.c_int, [vp, C.c_uint32, u32p, u32p, f64p, C.c_size_t, u32p, C.c_size_t]),
     "tfhe_gpu_keygen": (C.c_int, [vp, C.c_uint64, C.c_uint64, u32p, u32p, f64p, u32p]),
     "tfhe_gpu_key_blob_bytes": (C.c_int, [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
@@ -162,18 +177,76 @@ class TfheError(RuntimeError):
     pass
 
 
-class Context:
-    """One HIP device + its resident CloudKey (tfhe_gpu_ctx)."""
+def fft_tables(N: int = 1024, source: int = TWIDDLES_GLIBC):
+    """tfhe_fft_tables: (twist_re, twist_im, stage_re, stage_im) as the context builds them."""
+    lib = load_library()
+    t = [np.zeros(N // 2, np.float64), np.zeros(N // 2, np.float64), np.zeros(N // 2 - 1, np.float64),
+         np.zeros(N // 2 - 1, np.float64)]
+    rc = lib.tfhe_fft_tables(N, source, *[a.ctypes.data_as(f64p) for a in t])
+    if rc != 0:
+        raise TfheError(f"tfhe_fft_tables: status {rc}")
+    return tuple(t)
 
-    def __init__(self, params="128", device: int = 0):
+
+class Context:
+    """One HIP device + its resident CloudKey (tfhe_gpu_ctx), or with
+    `devices` a multi-device context (tfhe_gpu_create_multi): batches are
+    sharded over the devices, the key is broadcast once over RCCL."""
+
+    def __init__(self, params="128", device: int = 0, devices=None):
         self.lib = load_library()
         self.params = make_params(params) if not isinstance(params, TfheParams) else params
         h = vp()
-        rc = self.lib.tfhe_gpu_create(C.byref(self.params), device, C.byref(h))
+        if devices is None:
+            rc = self.lib.tfhe_gpu_create(C.byref(self.params), device, C.byref(h))
+            what = "tfhe_gpu_create"
+        else:
+            devs = (C.c_int * len(devices))(*devices)
+            rc = self.lib.tfhe_gpu_create_multi(C.byref(self.params), len(devices), devs, C.byref(h))
+            what = "tfhe_gpu_create_multi"
+            device = devices[0]
         if rc != 0:
-            raise TfheError(f"tfhe_gpu_create failed ({rc})")
+            raise TfheError(f"{what} failed ({rc})")
         self.h = h
         self.device = device
+
+    @classmethod
+    def multi(cls, params="128", num_devices: int = 1, devices=None):
+        return cls(params, devices=list(devices) if devices is not None else list(range(num_devices)))
+
+    @property
+    def num_devices(self) -> int:
+        return self.lib.tfhe_gpu_num_devices(self.h)
+
+    def set_option(self, name: str, value: int):
+        """tfhe_gpu_set_option (kernel forms, twiddle source; OPTIONS)."""
+        if name == "br_form" and isinstance(value, str):
+            value = BR_FORMS[value]
+        self.check(self.lib.tfhe_gpu_set_option(self.h, OPTIONS[name], int(value)), f"set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        self.check(self.lib.tfhe_gpu_get_option(self.h, OPTIONS[name], C.byref(v)), f"get_option({name})")
+        return v.value
+
+    def reset_options(self):
+        for k, v in OPTION_DEFAULTS.items():
+            if self.get_option(k) != v:
+                self.set_option(k, v)
+
+    @contextlib.contextmanager
+    def options(self, **kw):
+        """Temporarily set options (A/B runs, tests); defaults restored on exit."""
+        try:
+            for k, v in kw.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            self.reset_options()
+
+    def last_kernels(self) -> str:
+        """Kernel names of this context's last bootstrap launch (tfhe_gpu_last_kernels)."""
+        return self.lib.tfhe_gpu_last_kernels(self.h).decode()
 
     def close(self):
         if getattr(self, "h", None):
