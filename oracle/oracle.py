@@ -88,6 +88,9 @@ class Oracle:
                                            C.c_uint32, C.c_uint64, u32p]
         L.oracle_set_trig_source.argtypes = [C.c_int]
         L.oracle_get_trig_source.restype = C.c_int
+        L.oracle_take_round_error.restype = C.c_double
+        L.oracle_set_fused.argtypes = [C.c_int]
+        L.oracle_get_fused.restype = C.c_int
 
     # ---- cos/sin source of the twiddles (0 glibc, 1 fdlibm/musl; tfhe_oracle.c)
     def set_trig_source(self, source: int):
@@ -95,6 +98,14 @@ class Oracle:
 
     def trig_source(self) -> int:
         return self.lib.oracle_get_trig_source()
+
+    def set_fused(self, fused: bool):
+        """Arithmetic of the transforms / MAC: reference expression trees or fused multiply-adds."""
+        self.lib.oracle_set_fused(int(bool(fused)))
+
+    def take_round_error(self) -> float:
+        """max |x - round(x)| of the inverse transforms run on this thread since the last call."""
+        return self.lib.oracle_take_round_error()
 
     # ---- utils / fft
     def f64_to_torus(self, d: float) -> int:

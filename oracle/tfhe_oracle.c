@@ -232,6 +232,17 @@ static double tw_sin(double x) { return g_trig_source ? fd_sin(x) : sin(x); }
 double oracle_trig_cos(double x, int source) { return source == 1 ? fd_cos(x) : cos(x); }
 double oracle_trig_sin(double x, int source) { return source == 1 ? fd_sin(x) : sin(x); }
 
+/* Arithmetic of the transforms and the MAC: 0 = the reference's expression
+ * trees (default, fft.zig / trgsw.zig as written); 1 = "fused": every
+ * complex multiply-add as fused multiply-adds (a = u + x*w by two fma, the
+ * butterfly's b = 2u - a by one), the form the MI355X kernels use at the
+ * L=3 / Bg=2^6 sets (there the exact external product is an
+ * integer polynomial and both forms round to it).  Twiddle values and the
+ * operation order are unchanged.  Test infrastructure, like the rest. */
+static int g_fused = 0;
+void oracle_set_fused(int fused) { g_fused = fused ? 1 : 0; }
+int oracle_get_fused(void) { return g_fused; }
+
 /* ======================================================================== */
 /* FFT — fft.zig KlemsaProcessor                                             */
 /* ======================================================================== */
@@ -295,6 +306,14 @@ static void radix2_fft(cplx *data, size_t n, int inverse) {
             for (size_t j = 0; j < len / 2; j++) {
                 cplx u = data[i + j];
                 cplx x = data[i + j + len / 2];
+                if (g_fused) {                             /* a = u + x*w, b = 2u - a */
+                    double a_re = fma(x.re, w_re, fma(-x.im, w_im, u.re));
+                    double a_im = fma(x.re, w_im, fma(x.im, w_re, u.im));
+                    data[i + j].re = a_re;
+                    data[i + j].im = a_im;
+                    data[i + j + len / 2].re = fma(2.0, u.re, -a_re);
+                    data[i + j + len / 2].im = fma(2.0, u.im, -a_im);
+                } else {
                 cplx v;                                    /* Complex.mul :50-55 */
                 v.re = x.re * w_re - x.im * w_im;
                 v.im = x.re * w_im + x.im * w_re;
@@ -302,6 +321,7 @@ static void radix2_fft(cplx *data, size_t n, int inverse) {
                 data[i + j].im = u.im + v.im;
                 data[i + j + len / 2].re = u.re - v.re;
                 data[i + j + len / 2].im = u.im - v.im;
+                }
                 double temp = w_re * wlen_re - w_im * wlen_im;
                 w_im = w_re * wlen_im + w_im * wlen_re;
                 w_re = temp;
@@ -340,8 +360,13 @@ void oracle_ifft(uint32_t N, const uint32_t *in, double *out) {
         double in_re = (double)(int32_t)in[i];
         double in_im = (double)(int32_t)in[i + n2];
         double w_re = tre[i], w_im = tim[i];
-        buf[i].re = in_re * w_re - in_im * w_im;
-        buf[i].im = in_re * w_im + in_im * w_re;
+        if (g_fused) {
+            buf[i].re = fma(in_re, w_re, -(in_im * w_im));
+            buf[i].im = fma(in_re, w_im, in_im * w_re);
+        } else {
+            buf[i].re = in_re * w_re - in_im * w_im;
+            buf[i].im = in_re * w_im + in_im * w_re;
+        }
     }
     radix2_fft(buf, n2, 0);
     for (size_t i = 0; i < n2; i++) {
@@ -353,6 +378,17 @@ void oracle_ifft(uint32_t N, const uint32_t *in, double *out) {
 
 /* fft (frequency -> torus, the INVERSE transform) — fft.zig:207-246;
  * twin fft1024 :370-443. */
+/* Largest |value - nearest integer| the inverse transform has rounded on
+ * this thread since the last oracle_take_round_error() (test evidence for
+ * at the L=3 / Bg=2^6 sets the exact external product is an
+ * integer polynomial and the float error stays far below 1/2). */
+static __thread double tl_round_err = 0.0;
+double oracle_take_round_error(void) {
+    double e = tl_round_err;
+    tl_round_err = 0.0;
+    return e;
+}
+
 void oracle_fft(uint32_t N, const double *in, uint32_t *out) {
     size_t n2 = N / 2;
     cplx *buf = (cplx *)malloc(sizeof(cplx) * n2);
@@ -367,10 +403,13 @@ void oracle_fft(uint32_t N, const double *in, uint32_t *out) {
     for (size_t i = 0; i < n2; i++) {
         double w_re = tre[i], w_im = tim[i];
         double f_re = buf[i].re, f_im = buf[i].im;
-        double tmp_re = (f_re * w_re + f_im * w_im) * normalization;
-        double tmp_im = (f_im * w_re - f_re * w_im) * normalization;
+        double tmp_re = (g_fused ? fma(f_re, w_re, f_im * w_im) : f_re * w_re + f_im * w_im) * normalization;
+        double tmp_im = (g_fused ? fma(f_im, w_re, -(f_re * w_im)) : f_im * w_re - f_re * w_im) * normalization;
         int64_t rr = (int64_t)round(tmp_re);
         int64_t ri = (int64_t)round(tmp_im);
+        double e_re = fabs(tmp_re - round(tmp_re)), e_im = fabs(tmp_im - round(tmp_im));
+        if (e_re > tl_round_err) tl_round_err = e_re;
+        if (e_im > tl_round_err) tl_round_err = e_im;
         out[i] = (uint32_t)(int32_t)rr;
         out[i + n2] = (uint32_t)(int32_t)ri;
     }
@@ -447,6 +486,11 @@ void oracle_poly_mul_with_xk(uint32_t N, const uint32_t *a, uint32_t k, uint32_t
 static void fma_in_fd(size_t n2, double *res, const double *a, const double *b) {
     for (size_t i = 0; i < n2; i++) {
         double a_re = a[i], a_im = a[i + n2], b_re = b[i], b_im = b[i + n2];
+        if (g_fused) {  /* res += a*b*0.5 by fma; b*0.5 is exact */
+            res[i] = fma(a_re, b_re * 0.5, fma(-a_im, b_im * 0.5, res[i]));
+            res[i + n2] = fma(a_re, b_im * 0.5, fma(a_im, b_re * 0.5, res[i + n2]));
+            continue;
+        }
         double real_part = (a_re * b_re - a_im * b_im) * 0.5;
         res[i] = res[i] + real_part;
         double imag_part = (a_re * b_im + a_im * b_re) * 0.5;

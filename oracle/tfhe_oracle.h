@@ -142,6 +142,12 @@ void oracle_set_trig_source(int source);
 int oracle_get_trig_source(void);
 double oracle_trig_cos(double x, int source);
 double oracle_trig_sin(double x, int source);
+/* 0 = reference expression trees (default); 1 = fused multiply-adds (the
+ * MI355X kernels' form at the L=3 / Bg=2^6 sets) */
+void oracle_set_fused(int fused);
+int oracle_get_fused(void);
+/* max |x - round(x)| rounded by oracle_fft on this thread since the last call (then reset) */
+double oracle_take_round_error(void);
 
 #ifdef __cplusplus
 }
