@@ -108,9 +108,17 @@ enum {
     TFHE_OPT_KS_ITEM_GROUPS = 5,  /* basebit >= 5: item groups per block, 0 auto (4), 1, 2, 4, 8 */
     TFHE_OPT_KS_SEL_ITEMS = 6,    /* select / gather form: items per block, 8 (default), 16, 32 */
     TFHE_OPT_CIRCUIT_PACK = 7,    /* circuit_eval round packing: 1 (default), 0 off */
-    TFHE_OPT_TWIDDLES = 8         /* cos/sin source of the FFT tables: TFHE_TWIDDLES_* (set before a key
+    TFHE_OPT_TWIDDLES = 8,        /* cos/sin source of the FFT tables: TFHE_TWIDDLES_* (set before a key
                                      is generated: keygen transforms the key with these tables) */
+    TFHE_OPT_ARITH = 9            /* blind-rotation f64 arithmetic: TFHE_ARITH_* */
 };
+/* TFHE_ARITH_AUTO (default): where the exact external product is an integer
+ * polynomial the f64 evaluation rounds to (the L=3 / Bg=2^6 sets: the
+ * reference's own rounding error stays below ~0.1) the kernels
+ * use fused multiply-adds, which round to the same integers with fewer
+ * instructions; elsewhere (UINT4) the reference's expression trees.
+ * TFHE_ARITH_REFERENCE: the reference's expression trees everywhere. */
+enum { TFHE_ARITH_AUTO = 0, TFHE_ARITH_REFERENCE = 1 };
 /* The two libm candidates a Zig build of the reference can bind @cos/@sin to
  * (fft.zig:98-106, :591-593): glibc (linkLibC on Linux) or Zig's compiler_rt
  * port of the fdlibm/musl kernels.  DESIGN.md §6 lists the entries where the

@@ -93,19 +93,23 @@ def test_key_switch_vs_oracle(oracle, pname, B, form):
 
 
 # ---- blind rotation / bootstrap ---------------------------------------------
-@pytest.mark.parametrize("form", ["whole", "whole-noloader", "split", "wide"])
+@pytest.mark.parametrize("form", ["whole", "whole-noloader", "whole-reference", "whole-noloader-reference",
+                                  "split", "wide"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
 def test_blind_rotate_vs_oracle(oracle, pname, B, form):
-    """All kernel forms (1 wave per item with or without loader waves / 2 waves
-    per item / 8 waves per item) bit-exact."""
+    """All kernel forms (1 wave per item with or without loader waves, fused or
+    reference arithmetic / 2 waves per item / 8 waves per item) bit-exact."""
     c, k = ctx_for(oracle, pname)
     cts = u32rand(rng(6), B, k.p.n + 1)  # uniform TLWE: bit-exactness only
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
     # odd batch sizes leave idle item slots in the last workgroup
     cts5 = u32rand(rng(16), 5, k.p.n + 1)
     want5 = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts5])
-    with c.options(br_form=form.split("-")[0], br_loader=int(not form.endswith("noloader"))):
+    with c.options(br_form=form.split("-")[0], br_loader=int("noloader" not in form),
+                   arith=int(form.endswith("reference"))):
         assert np.array_equal(c.blind_rotate_batch(cts), want)
+        if form.startswith("whole"):  # fused arithmetic only where the external product is exact (SMALL)
+            assert c.last_kernels().endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
         assert c.last_kernels().startswith({"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<",
                                             "wide": "k_blind_rotate_wide<"}[form.split("-")[0]])
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
@@ -401,6 +405,33 @@ def test_gates128_fdlibm_golden_fixture():
     out = c.gate_batch(g["ops"], g["a"], g["b"])
     assert hashlib.sha256(np.ascontiguousarray(out, np.uint32).tobytes()).hexdigest() == str(g["out_sha256"])
     c.close()
+
+
+def test_fused_and_reference_arithmetic_agree_1024(oracle):
+    """The headline shape (1,024 NAND, 128-bit, whole form): the fused-multiply-add
+    kernel and the reference-expression-tree kernel give identical words for every
+    gate (each CMUX rounds the same exact integer polynomial), and a sample is
+    bit-exact vs the oracle in both of its arithmetic modes."""
+    c, k = ctx_for(oracle, "128")
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    g = rng(93)
+    a_bits, b_bits = g.integers(0, 2, 1024).astype(np.uint8), g.integers(0, 2, 1024).astype(np.uint8)
+    A, B = sk.encrypt_bool(a_bits, seed0=93_000), sk.encrypt_bool(b_bits, seed0=94_000)
+    ops = np.zeros(1024, np.uint8)
+    fused = c.gate_batch(ops, A, B)
+    assert "fused" in c.last_kernels()
+    with c.options(arith=tfhe_amd.ARITH_REFERENCE):
+        ref = c.gate_batch(ops, A, B)
+        assert "fused" not in c.last_kernels()
+    assert np.array_equal(fused, ref)
+    idx = np.array([0, 511, 1023])
+    for mode in (0, 1):
+        try:
+            oracle.set_fused(mode)
+            want = oracle.gate_batch(k.p, ops[idx], A[idx], B[idx], k.ck, threads=3)
+        finally:
+            oracle.set_fused(0)
+        assert np.array_equal(fused[idx], want)
 
 
 def test_options_validation_and_report(oracle):

@@ -184,6 +184,44 @@ def test_external_product_is_exact_integer(oracle, pname):
             oracle.set_trig_source(0)
 
 
+@pytest.mark.parametrize("pname", ["128", "80"])
+def test_fused_arithmetic_rounds_to_the_same_integers(oracle, pname):
+    """The oracle's fused mode (the MI355X kernels' fused multiply-adds) and its
+    reference mode give identical blind rotations at the L=3 / Bg=2^6 sets, and
+    each rounds values within 0.15 of an integer (the measured margin is ~0.09;
+    a mismatch needs an error of 1/2)."""
+    k = get_keys(oracle, pname)
+    g = rng(95)
+    for _ in range(2):
+        ct = g.integers(0, 1 << 32, k.p.n + 1, dtype=np.uint64).astype(np.uint32)
+        oracle.take_round_error()
+        a = oracle.blind_rotate(k.p, ct, k.ck.testvec, k.ck.bk, k.ck.offset)
+        e_ref = oracle.take_round_error()
+        try:
+            oracle.set_fused(1)
+            b = oracle.blind_rotate(k.p, ct, k.ck.testvec, k.ck.bk, k.ck.offset)
+            e_fu = oracle.take_round_error()
+        finally:
+            oracle.set_fused(0)
+        assert np.array_equal(a, b)
+        assert e_ref < 0.15 and e_fu < 0.15
+
+
+def test_fused_arithmetic_differs_where_inexact(oracle, keys_uint4):
+    """UINT4 (Bg = 2^22): products pass 2^53, the rounding is the result, the two
+    arithmetic modes differ, so the kernels keep the reference's trees there."""
+    k = keys_uint4
+    ct = rng(96).integers(0, 1 << 32, k.p.n + 1, dtype=np.uint64).astype(np.uint32)
+    a = oracle.blind_rotate(k.p, ct, k.ck.testvec, k.ck.bk, k.ck.offset)
+    assert oracle.take_round_error() >= 0.5
+    try:
+        oracle.set_fused(1)
+        b = oracle.blind_rotate(k.p, ct, k.ck.testvec, k.ck.bk, k.ck.offset)
+    finally:
+        oracle.set_fused(0)
+    assert not np.array_equal(a, b)
+
+
 def test_twiddle_source_changes_gates_only_where_inexact():
     """Committed evidence (tests/golden/make_golden.py): the 128-bit gate fixture is
     bit-identical under the glibc and the fdlibm twiddles (exact external products),

@@ -58,6 +58,8 @@ struct LaunchOpts {
     int ks_narrow = 0;   // basebit 2: 1 forces the 32-word x 4-wave blocks
     int ks_groups = 0;   // basebit >= 5: item groups per block (0 auto = 4; 1, 2, 4, 8)
     int ks_sel_items = 8;  // select/gather form: items per block (8, 16, 32)
+    int arith_strict = 0;  // 1: the reference's f64 expression trees even where fused multiply-adds round
+                           // to the same integers (the L=3 / Bg=2^6 sets)
 };
 
 // ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------

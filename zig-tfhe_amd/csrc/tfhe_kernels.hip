@@ -73,9 +73,28 @@ DEV C2 twmul(C2 a, C2 w) {
     return c2(a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y);
 }
 
+// Fused arithmetic (FU = true).  At the L=3 / Bg=2^6 sets the
+// exact external product is an integer polynomial and the reference's f64
+// evaluation stays within ~0.09 of it (oracle_take_round_error), so any
+// evaluation with an error below 1/2 rounds to the same integers.  FU kernels
+// evaluate every complex multiply-add with fused multiply-adds, in the
+// reference's operation order with the reference's twiddles: a butterfly is
+// a = u + x*w (two fma) and b = 2u - a (one fma), 6 ops instead of 10; a MAC
+// term is two fma per component.  The oracle's fused mode (oracle_set_fused)
+// restates exactly these expressions.  Never used where products exceed 2^53
+// (UINT4: SMALL = false), where the reference's rounding is the result.
+DEV double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
 // radix2FFT inner butterfly (fft.zig:600-606)
-template <bool INV>
+template <bool INV, bool FU = false>
 DEV void bf(C2 &u, C2 &x, C2 w) {
+    if (FU) {  // x*w for the forward twiddle, x*conj(w) for INV
+        const double ax = INV ? fmad(x.x, w.x, fmad(x.y, w.y, u.x)) : fmad(x.x, w.x, fmad(-x.y, w.y, u.x));
+        const double ay = INV ? fmad(-x.x, w.y, fmad(x.y, w.x, u.y)) : fmad(x.x, w.y, fmad(x.y, w.x, u.y));
+        x = c2(fmad(2.0, u.x, -ax), fmad(2.0, u.y, -ay));
+        u = c2(ax, ay);
+        return;
+    }
     C2 v = twmul<INV>(x, w);
     C2 a = c2(u.x + v.x, u.y + v.y);
     C2 b = c2(u.x - v.x, u.y - v.y);
@@ -83,8 +102,16 @@ DEV void bf(C2 &u, C2 &x, C2 w) {
     x = b;
 }
 // j == 0 butterfly: the recurrence twiddle is exactly (1, 0); x*(1,0) == x up
-// to the sign of zero, which never reaches an output integer.
+// to the sign of zero, which never reaches an output integer.  FU: a = u + x
+// is the fused form's a exactly, b = 2u - a as in every fused butterfly.
+template <bool FU = false>
 DEV void bf1(C2 &u, C2 &x) {
+    if (FU) {
+        const C2 a = c2(u.x + x.x, u.y + x.y);
+        x = c2(fmad(2.0, u.x, -a.x), fmad(2.0, u.y, -a.y));
+        u = a;
+        return;
+    }
     C2 a = c2(u.x + x.x, u.y + x.y);
     C2 b = c2(u.x - x.x, u.y - x.y);
     u = a;
@@ -96,8 +123,15 @@ DEV void bf1(C2 &u, C2 &x) {
 // the tables are built, tfhe_gpu.cpp): x.y * -1.0 == -x.y exactly, so the
 // reference's products by w.y are sign flips folded into the adds.  Same
 // results as bf<INV>(u, x, (wx, -1.0)) bit for bit, two multiplies fewer.
-template <bool INV>
+template <bool INV, bool FU = false>
 DEV void bf_m1(C2 &u, C2 &x, double wx) {
+    if (FU) {  // the fused butterfly with w.y = -1: x.y * -1 and x.x * -1 are exact
+        const double ax = INV ? fmad(x.x, wx, u.x - x.y) : fmad(x.x, wx, u.x + x.y);
+        const double ay = INV ? fmad(x.y, wx, u.y) + x.x : fmad(x.y, wx, u.y) - x.x;
+        x = c2(fmad(2.0, u.x, -ax), fmad(2.0, u.y, -ay));
+        u = c2(ax, ay);
+        return;
+    }
     const C2 v = INV ? c2(x.x * wx - x.y, x.y * wx + x.x) : c2(x.x * wx + x.y, x.y * wx - x.x);
     C2 a = c2(u.x + v.x, u.y + v.y);
     C2 b = c2(u.x - v.x, u.y - v.y);
@@ -173,20 +207,20 @@ struct LdsTw {
 
 // Pass A: stages len = 2, 4, 8 (bits 0-2 of the bit-reversed position are the
 // register index q).
-template <bool INV>
+template <bool INV, bool FU = false>
 DEV void passA(C2 *d, const C2 *a) {
-    bf1(d[0], d[1]); bf1(d[2], d[3]); bf1(d[4], d[5]); bf1(d[6], d[7]);
-    bf1(d[0], d[2]); bf_m1<INV>(d[1], d[3], a[0].x); bf1(d[4], d[6]); bf_m1<INV>(d[5], d[7], a[0].x);
-    bf1(d[0], d[4]); bf<INV>(d[1], d[5], a[1]); bf_m1<INV>(d[2], d[6], a[2].x); bf<INV>(d[3], d[7], a[3]);
+    bf1<FU>(d[0], d[1]); bf1<FU>(d[2], d[3]); bf1<FU>(d[4], d[5]); bf1<FU>(d[6], d[7]);
+    bf1<FU>(d[0], d[2]); bf_m1<INV, FU>(d[1], d[3], a[0].x); bf1<FU>(d[4], d[6]); bf_m1<INV, FU>(d[5], d[7], a[0].x);
+    bf1<FU>(d[0], d[4]); bf<INV, FU>(d[1], d[5], a[1]); bf_m1<INV, FU>(d[2], d[6], a[2].x); bf<INV, FU>(d[3], d[7], a[3]);
 }
 // Pass B: stages 16, 32, 64 (position bits 3-5 in q; j = (t&7) + 8*(...)).
 // Pass C: stages 128, 256, 512 (position bits 6-8 in q; j = t + 64*(...)).
 // w = {W_s1, W_s2[0..1], W_s3[0..3]} of the pass's three stages.
-template <bool INV>
+template <bool INV, bool FU = false>
 DEV void passBC(C2 *d, const C2 *w) {
-    bf<INV>(d[0], d[1], w[0]); bf<INV>(d[2], d[3], w[0]); bf<INV>(d[4], d[5], w[0]); bf<INV>(d[6], d[7], w[0]);
-    bf<INV>(d[0], d[2], w[1]); bf<INV>(d[1], d[3], w[2]); bf<INV>(d[4], d[6], w[1]); bf<INV>(d[5], d[7], w[2]);
-    bf<INV>(d[0], d[4], w[3]); bf<INV>(d[1], d[5], w[4]); bf<INV>(d[2], d[6], w[5]); bf<INV>(d[3], d[7], w[6]);
+    bf<INV, FU>(d[0], d[1], w[0]); bf<INV, FU>(d[2], d[3], w[0]); bf<INV, FU>(d[4], d[5], w[0]); bf<INV, FU>(d[6], d[7], w[0]);
+    bf<INV, FU>(d[0], d[2], w[1]); bf<INV, FU>(d[1], d[3], w[2]); bf<INV, FU>(d[4], d[6], w[1]); bf<INV, FU>(d[5], d[7], w[2]);
+    bf<INV, FU>(d[0], d[4], w[3]); bf<INV, FU>(d[1], d[5], w[4]); bf<INV, FU>(d[2], d[6], w[5]); bf<INV, FU>(d[3], d[7], w[6]);
 }
 
 // Exchange 1 (after pass A): lane t wrote positions 8*br6(t)+q, reads
@@ -269,31 +303,31 @@ DEV void ex2_read(C2 *d, const C2 *xb, int t) {
 // ONEBUF: both transforms exchange through one 8 KB buffer.  Every write
 // into it follows, in this wave's program order, the reads of the data it
 // overwrites, and one wave's LDS operations execute in order.
-template <bool INV, bool ONEBUF = false, class TW>
+template <bool INV, bool ONEBUF = false, bool FU = false, class TW>
 DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     C2 *x0 = xb, *x1 = ONEBUF ? xb : xb + 512;
     C2 wb_[7], wc_[7];
-    passA<INV>(d[0], T.a);
+    passA<INV, FU>(d[0], T.a);
     ex1_write(d[0], x0, t);
     wave_sync();
-    passA<INV>(d[1], T.a);
+    passA<INV, FU>(d[1], T.a);
     ex1_read(d[0], x0, t);
     ex1_write(d[1], x1, t);
     wave_sync();
     T.pass_b(wb_, t);
-    passBC<INV>(d[0], wb_);
+    passBC<INV, FU>(d[0], wb_);
     ex1_read(d[1], x1, t);
     ex2_write(d[0], x0, t);
     wave_sync();
-    passBC<INV>(d[1], wb_);
+    passBC<INV, FU>(d[1], wb_);
     T.pass_c(wc_, t);
     ex2_read(d[0], x0, t);
     ex2_write(d[1], x1, t);
     wave_sync();
-    passBC<INV>(d[0], wc_);
+    passBC<INV, FU>(d[0], wc_);
     ex2_read(d[1], x1, t);
     wave_sync();
-    passBC<INV>(d[1], wc_);
+    passBC<INV, FU>(d[1], wc_);
 }
 
 template <int NF, bool INV, class TW>
@@ -317,7 +351,11 @@ DEV void fft512(C2 (*d)[8], C2 *xb, const TW &T, int t) {
 }
 
 // Fold + twist of ifft1024 (fft.zig:301-323): z = (x_re, x_im) * twist.
-DEV C2 twist_in(double xr, double xi, C2 w) { return c2(xr * w.x - xi * w.y, xr * w.y + xi * w.x); }
+template <bool FU = false>
+DEV C2 twist_in(double xr, double xi, C2 w) {
+    if (FU) return c2(fmad(xr, w.x, -(xi * w.y)), fmad(xr, w.y, xi * w.x));
+    return c2(xr * w.x - xi * w.y, xr * w.y + xi * w.x);
+}
 
 // Untwist + normalisation of fft1024 (fft.zig:412-429).  `f` is 2x the
 // reference's value (the ×0.5 input scaling is folded), hence 1/(2*512).
@@ -325,11 +363,16 @@ DEV C2 twist_in(double xr, double xi, C2 w) { return c2(xr * w.x - xi * w.y, xr 
 // scaled by 2^-10 (k_bk_permute); a power-of-two factor commutes with every
 // rounded add and multiply of the MAC, the inverse FFT and the untwist (no
 // overflow or subnormal at these magnitudes), so the results are identical.
-template <bool NORM = true>
+template <bool NORM = true, bool FU = false>
 DEV void untwist_out(C2 f, C2 w, double &tr, double &ti) {
     const double norm = 1.0 / 1024.0;
-    tr = f.x * w.x + f.y * w.y;
-    ti = f.y * w.x - f.x * w.y;
+    if (FU) {
+        tr = fmad(f.x, w.x, f.y * w.y);
+        ti = fmad(f.y, w.x, -(f.x * w.y));
+    } else {
+        tr = f.x * w.x + f.y * w.y;
+        ti = f.y * w.x - f.x * w.y;
+    }
     if (NORM) {
         tr = tr * norm;
         ti = ti * norm;
@@ -446,6 +489,7 @@ DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t) {
 // the 4 BK words of group q+1 are read while group q's 32 flops issue, and a
 // scheduling fence per group keeps hipcc from hoisting all 32 reads (128
 // VGPRs) ahead of the arithmetic, which pushes the kernel into AGPR copies.
+template <bool FU = false>
 DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 *bk, int t) {
     double2 k[2][4];
     k[0][0] = bk[t];
@@ -465,6 +509,11 @@ DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 
         for (int r = 0; r < 2; r++) {
             const C2 x = r ? d1[q] : d0[q];
             const double2 ka = k[c][2 * r], kb = k[c][2 * r + 1];
+            if (FU) {  // acc += x*k: two fma per component (oracle fused fma_in_fd)
+                fa[q] = c2(fmad(x.x, ka.x, fmad(-x.y, ka.y, fa[q].x)), fmad(x.x, ka.y, fmad(x.y, ka.x, fa[q].y)));
+                fb[q] = c2(fmad(x.x, kb.x, fmad(-x.y, kb.y, fb[q].x)), fmad(x.x, kb.y, fmad(x.y, kb.x, fb[q].y)));
+                continue;
+            }
             const C2 ta = c2(x.x * ka.x - x.y * ka.y, x.x * ka.y + x.y * ka.x);
             const C2 tb = c2(x.x * kb.x - x.y * kb.y, x.x * kb.y + x.y * kb.x);
             fa[q] = c2(fa[q].x + ta.x, fa[q].y + ta.y);
@@ -476,7 +525,7 @@ DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 
 
 // Inverse transforms of the two accumulated spectra (fft1024 x2) and the
 // CMUX add acc' = ExtProd + acc (trgsw.zig:277-281), lane-local.
-template <bool SMALL, int TS, bool ONEBUF = false, class TW>
+template <bool SMALL, int TS, bool ONEBUF = false, bool FU = false, class TW>
 DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const C2 *tws, int t,
                          uint32_t *accA, uint32_t *accB) {
     C2 e[2][8];
@@ -486,14 +535,14 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
         e[1][q] = fb[br3(q)];
     }
 #ifndef TFHE_KO_INV
-    fft512_x2<true, ONEBUF>(e, xb, T, t);
+    fft512_x2<true, ONEBUF, FU>(e, xb, T, t);
 #endif
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         double ra, ia, rb, ib;
         const C2 w = tws[q * TS];
-        untwist_out<false>(e[0][q], w, ra, ia);
-        untwist_out<false>(e[1][q], w, rb, ib);
+        untwist_out<false, FU>(e[0][q], w, ra, ia);
+        untwist_out<false, FU>(e[1][q], w, rb, ib);
         accA[q] += to_torus<SMALL>(ra);
         accA[q + 8] += to_torus<SMALL>(ia);
         accB[q] += to_torus<SMALL>(rb);
@@ -586,6 +635,7 @@ DEV void load_digits_lds(C2 *d, const uint32_t *s_tmp, int row, int L, int bgbit
 }
 
 // Digits of rows (row, row+1) with one read of the 8 twist factors for both.
+template <bool FU = false>
 DEV void load_digits_pair_lds(C2 (*d)[8], const uint32_t *s_tmp, int row, int L, int bgbit, const C2 *twist_t,
                               int t) {
     const uint32_t *src[2];
@@ -602,8 +652,8 @@ DEV void load_digits_pair_lds(C2 (*d)[8], const uint32_t *s_tmp, int row, int L,
         const C2 w = twist_t[64 * m];
 #pragma unroll
         for (int f = 0; f < 2; f++)
-            d[f][q] = twist_in(digit_f64(src[f][64 * m], level[f], bgbit), digit_f64(src[f][64 * (m + 8)], level[f], bgbit),
-                               w);
+            d[f][q] = twist_in<FU>(digit_f64(src[f][64 * m], level[f], bgbit),
+                                   digit_f64(src[f][64 * (m + 8)], level[f], bgbit), w);
     }
 }
 
@@ -627,7 +677,7 @@ DEV void issue_bk_pair_async(const double2 *__restrict__ src, double2 *slot, int
     }
 }
 
-template <int L, bool LOADER>
+template <int L, bool LOADER, bool FU = false>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
                   PhaseProf &pp) {
@@ -640,9 +690,9 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
     for (int rp = 0; rp < L; rp++) {
         C2 d[2][8];
         pp.mark(1);
-        load_digits_pair_lds(d, s_tmp, 2 * rp, L, bgbit, twist_t, t);
+        load_digits_pair_lds<FU>(d, s_tmp, 2 * rp, L, bgbit, twist_t, t);
 #ifndef TFHE_KO_FFT  // TFHE_KO_*: development knock-out builds (timing only)
-        fft512_x2<false, true>(d, xb, T, t);
+        fft512_x2<false, true, FU>(d, xb, T, t);
 #endif
         pp.mark(2);
         const int slot = (slot0 + rp) & 1;
@@ -659,7 +709,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #endif
         pp.mark(3);
 #ifndef TFHE_KO_MAC
-        mac_pair_lds(fa, fb, d[0], d[1], s_bk + slot * 2048, t);
+        mac_pair_lds<FU>(fa, fb, d[0], d[1], s_bk + slot * 2048, t);
 #else
         for (int q = 0; q < 8; q++) fa[q] = c2(fa[q].x + d[0][q].x, fa[q].y + d[1][q].y);
 #endif
@@ -670,7 +720,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 // LOADER: 4 more waves per workgroup, one beside each gate's wave on its SIMD,
 // issue the BK row-pair DMAs (the same pieces, slots and barriers), so the
 // gate waves only compute.
-template <int L, bool SMALL, bool LOADER = false>
+template <int L, bool SMALL, bool LOADER = false, bool FU = false>
 __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
@@ -796,10 +846,10 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         wave_sync();
         C2 fa[8], fb[8];
         at_next = s_at[i + 1 < n ? i + 1 : i];
-        br_pairs<L, LOADER>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
-                    bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp);
+        br_pairs<L, LOADER, FU>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
+                                bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp);
         pp.mark(5);
-        inverse_and_add<SMALL, 64, true>(fa, fb, s_x, T, twist_t, t, accA, accB);
+        inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB);
         wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) {
@@ -1647,6 +1697,9 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     const bool split = form == 's';
     const bool wide = form == 'W';
     const bool loader = !wide && !split && O.br_loader != 0;
+    // fused arithmetic in the exact-integer regime (SMALL) unless the
+    // reference expression trees are requested (TFHE_OPT_ARITH)
+    const bool fused = small && O.arith_strict == 0;
     dim3 grid, block;
     if (wide) {
         grid = dim3((unsigned)B);
@@ -1668,14 +1721,22 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
             hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
                                testvec, bk2, out, out_mode, B);                                                   \
             if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ "> (split form)";                               \
-        } else if (loader) {                                                                                      \
-            hipLaunchKernelGGL((k_blind_rotate<L_, S_, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
+        } else if (loader && fused) {                                                                             \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, \
                                testvec, bk2, out, out_mode, B);                                                   \
-            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true> (whole form, loader waves)";                  \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true,true> (whole form, loader waves, fused)";      \
+        } else if (loader) {                                                                                      \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, false>), grid, block, 0, s, P, T, ops, in_a, in_b,   \
+                               idx, testvec, bk2, out, out_mode, B);                                              \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true,false> (whole form, loader waves)";            \
+        } else if (fused) {                                                                                       \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_, false, S_>), grid, block, 0, s, P, T, ops, in_a, in_b,     \
+                               idx, testvec, bk2, out, out_mode, B);                                              \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",false,true> (whole form, fused)";                   \
         } else {                                                                                                  \
-            hipLaunchKernelGGL((k_blind_rotate<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,  \
-                               bk2, out, out_mode, B);                                                            \
-            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",false> (whole form)";                               \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_, false, false>), grid, block, 0, s, P, T, ops, in_a, in_b,  \
+                               idx, testvec, bk2, out, out_mode, B);                                              \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",false,false> (whole form)";                         \
         }                                                                                                         \
     } while (0)
     switch (P.L) {
