@@ -62,14 +62,20 @@ def algorithmic_bytes_per_gate(p) -> int:
     return p.n * 2 * p.L * 2 * p.N * 8 + 2 * (p.n + 1) * 4 + (p.N + 1) * 4
 
 
-def f64_ops_per_cmux(L: int) -> int:
-    """Algorithmic f64 adds+muls of one CMUX (no FMA: the reference's
-    expression trees), excluding torus conversion: 2L forward + 2 inverse
-    512-point radix-2 FFTs (1,793 non-trivial butterflies x 4 mul + 2 add,
-    2,304 x 4 add), 2L twists + 2 untwists (4 mul + 2 add per point, + the
-    1/1024 norm), 2L x 2 x 512 complex MACs (4 mul + 4 add).  L=3: 235,568;
-    matches SQ_INSTS_VALU_{ADD,MUL}_F64 x 64 to within the conversion adds
-    (profiles/r01_pmc_blind_rotate_whole.txt)."""
+def f64_ops_per_cmux(L: int, fused: bool = False) -> int:
+    """f64 VALU lane-operations (v_add/v_mul/v_fma_f64, one each) of one CMUX,
+    excluding the torus conversion.
+    Reference expression trees (fused=False; the reference's adds+muls): 2L
+    forward + 2 inverse 512-point radix-2 FFTs (1,793 butterflies with a
+    twiddle x 4 mul + 2 add, 2,304 x 4 add), 2L twists + 2 untwists (4 mul + 2 add
+    per point, + the 1/1024 norm), 2L x 2 x 512 complex MACs (4 mul + 4 add).
+    L=3: 235,568; matched SQ_INSTS_VALU_{ADD,MUL}_F64 x 64 (profiles/r02a_pmc_blind_rotate.json).
+    Fused (the kernels' default at the L=3 / Bg=2^6 sets): a butterfly with a
+    twiddle is 6 fma, a j = 0 one 2 add + 2 fma, a twist / untwist point 2 mul +
+    2 fma (norm folded), a MAC term 4 fma.  L=3: 143,376."""
+    if fused:
+        per_fft = 511 * 4 + 1793 * 6
+        return (2 * L + 2) * per_fft + 2 * L * 512 * 4 + 2 * 512 * 4 + 2 * L * 2 * 512 * 4
     fft_mul, fft_add = 1793 * 4, 1793 * 2 + 2304 * 4
     fwd, inv = 2 * L, 2
     mul = (fwd + inv) * fft_mul + fwd * 2048 + inv * (2048 + 1024) + 2 * L * 2 * 512 * 4
@@ -77,7 +83,7 @@ def f64_ops_per_cmux(L: int) -> int:
     return mul + add
 
 
-VALU_F64_PEAK = 256 * 4 * 16 * 2.4e9  # non-FMA f64 ops/s: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz (78.6 TF FMA spec / 2)
+VALU_F64_PEAK = 256 * 4 * 16 * 2.4e9  # f64 VALU lane-ops/s: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz (78.6 TF FMA spec / 2)
 # measured with tools/isa_rate.hip (profiles/r01_isa_rate.txt): independent v_add_f64 / v_mul_f64
 # at 4 waves per SIMD issue every 2.01 ns per SIMD -> 1024 SIMDs x 64 lanes / 2.01 ns
 VALU_F64_SUSTAINED = 1024 * 64 / 2.01e-9
@@ -161,24 +167,31 @@ def pmc_record(batch: int, params: str):
 
 def rooflines(p, B, params, br_avg_s, kernel):
     """Primary roofline: f64 VALU issue, the bound the blind rotation is on (its
-    HBM traffic is ~60 GB/s); the SURVEY §8d streamed-key figure beside it."""
-    ops = f64_ops_per_cmux(p.L) * p.n * B
+    HBM traffic is ~60 GB/s): the kernel's f64 VALU lane-operations (model
+    f64_ops_per_cmux, checked against the PMC instruction counts) per second vs
+    the chip's issue rate; the SURVEY §8d streamed-key figure beside it."""
+    fused = "fused" in kernel
+    per_cmux = f64_ops_per_cmux(p.L, fused)
+    ops = per_cmux * p.n * B
     f64_rate = ops / br_avg_s
     pmc, why = pmc_record(B, params)
     roof = {"bound": "valu_f64", "achieved": round(f64_rate / 1e12, 3), "peak": round(VALU_F64_PEAK / 1e12, 1),
-            "unit": "Tops/s (f64 add+mul, no FMA)", "frac": round(f64_rate / VALU_F64_PEAK, 4),
+            "unit": "T f64 VALU lane-ops/s (v_add/v_mul/v_fma_f64 count one each)",
+            "frac": round(f64_rate / VALU_F64_PEAK, 4),
             "peak_sustained": round(VALU_F64_SUSTAINED / 1e12, 1),
             "frac_sustained": round(f64_rate / VALU_F64_SUSTAINED, 4),
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "kernel": kernel, "kernel_avg_ms": round(br_avg_s * 1e3, 3),
-            "algorithmic_f64_ops_per_launch": ops,
-            "f64_ops_per_cmux": f64_ops_per_cmux(p.L)}
+            "algorithmic_f64_ops_per_launch": ops, "f64_ops_per_cmux": per_cmux,
+            "arithmetic": "fused multiply-add (exact-integer regime, DESIGN.md §6)" if fused else "reference expression trees",
+            "reference_tree_f64_ops_per_cmux": f64_ops_per_cmux(p.L)}
     if pmc:
         roof["pmc"] = {k: pmc[k] for k in ("valu_f64_insts_per_launch", "valu_insts_per_gate_wave_per_cmux",
                                            "lds_insts_per_gate_wave_per_cmux", "wait_any_frac_gate_waves")
                        if k in pmc}
-        if pmc.get("valu_f64_insts_per_launch"):
-            roof["pmc"]["valu_f64_frac_from_pmc"] = round(pmc["valu_f64_insts_per_launch"] * 64 / br_avg_s / VALU_F64_PEAK, 4)
+        f64_insts = pmc.get("valu_f64_insts_per_launch", 0) + pmc.get("valu_fma_f64_insts_per_launch", 0)
+        if f64_insts:
+            roof["pmc"]["valu_f64_frac_from_pmc"] = round(f64_insts * 64 / br_avg_s / VALU_F64_PEAK, 4)
     else:
         roof["traffic_note"] = why
     alg = algorithmic_bytes_per_gate(p) * B

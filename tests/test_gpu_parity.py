@@ -446,4 +446,7 @@ def test_options_validation_and_report(oracle):
     g = rng(91)
     cts = u32rand(g, 3, k.p.n + 1)
     c.bootstrap_batch(cts)
-    assert c.last_kernels() == "k_blind_rotate_wide<3,true> (latency form) + k_key_switch_lanes<9,2,32,4,1>"
+    assert c.last_kernels() == "k_blind_rotate_wide<3,true,true> (latency form, fused) + k_key_switch_lanes<9,2,32,4,1>"
+    with c.options(arith=tfhe_amd.ARITH_REFERENCE):
+        c.bootstrap_batch(cts)
+        assert c.last_kernels() == "k_blind_rotate_wide<3,true,false> (latency form) + k_key_switch_lanes<9,2,32,4,1>"

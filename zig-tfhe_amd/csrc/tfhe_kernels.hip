@@ -330,23 +330,23 @@ DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     passBC<INV, FU>(d[1], wc_);
 }
 
-template <int NF, bool INV, class TW>
+template <int NF, bool INV, bool FU = false, class TW>
 DEV void fft512(C2 (*d)[8], C2 *xb, const TW &T, int t) {
 #pragma unroll
-    for (int f = 0; f < NF; f++) passA<INV>(d[f], T.a);
+    for (int f = 0; f < NF; f++) passA<INV, FU>(d[f], T.a);
     exchange1<NF>(d, xb, t);
     {
         C2 w[7];
         T.pass_b(w, t);
 #pragma unroll
-        for (int f = 0; f < NF; f++) passBC<INV>(d[f], w);
+        for (int f = 0; f < NF; f++) passBC<INV, FU>(d[f], w);
     }
     exchange2<NF>(d, xb, t);
     {
         C2 w[7];
         T.pass_c(w, t);
 #pragma unroll
-        for (int f = 0; f < NF; f++) passBC<INV>(d[f], w);
+        for (int f = 0; f < NF; f++) passBC<INV, FU>(d[f], w);
     }
 }
 
@@ -917,10 +917,15 @@ DEV void issue_bk_rows(const double2 *__restrict__ rows, double2 *lds, int tid) 
                                          (lds_void_t *)(lds + 512 * c + wbase), 16, 0, 0);
 }
 
-// term = D * BK row part (fmaInFd1024's (a_re*b_re - a_im*b_im, a_re*b_im + a_im*b_re))
-DEV C2 cmul_bk(C2 d, double2 k) { return c2(d.x * k.x - d.y * k.y, d.x * k.y + d.y * k.x); }
+// term = D * BK row part (fmaInFd1024's (a_re*b_re - a_im*b_im, a_re*b_im + a_im*b_re));
+// FU: one multiply and one fma per component
+template <bool FU = false>
+DEV C2 cmul_bk(C2 d, double2 k) {
+    if (FU) return c2(fmad(d.x, k.x, -(d.y * k.y)), fmad(d.x, k.y, d.y * k.x));
+    return c2(d.x * k.x - d.y * k.y, d.x * k.y + d.y * k.x);
+}
 
-template <int L, bool SMALL>
+template <int L, bool SMALL, bool FU = false>
 __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
@@ -1003,11 +1008,11 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int m = br3(q);
-                d[0][q] = twist_in(digit_f64(src[64 * m], level, P.bgbit),
+                d[0][q] = twist_in<FU>(digit_f64(src[64 * m], level, P.bgbit),
                                    digit_f64(src[64 * (m + 8)], level, P.bgbit), twist_t[64 * m]);
             }
 #ifndef TFHE_KO_FFT
-            fft512<1, false>(d, s_x, T, t);
+            fft512<1, false, FU>(d, s_x, T, t);
 #endif
 #pragma unroll
             for (int q = 0; q < 8; q++) s_x[t + 64 * q] = d[0][q];  // publish this row's spectrum
@@ -1017,8 +1022,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
 #ifndef TFHE_KO_MAC
 #pragma unroll
             for (int q = 0; q < 8; q++) {
-                const C2 t0 = cmul_bk(spec_0[t + 64 * q], s_bk[(2 * q + h) * 64 + t]);
-                const C2 t1 = cmul_bk(spec_1[t + 64 * q], s_bk[1024 + (2 * q + h) * 64 + t]);
+                const C2 t0 = cmul_bk<FU>(spec_0[t + 64 * q], s_bk[(2 * q + h) * 64 + t]);
+                const C2 t1 = cmul_bk<FU>(spec_1[t + 64 * q], s_bk[1024 + (2 * q + h) * 64 + t]);
                 S[q] = c2(S[q].x + t0.x, S[q].y + t0.y);
                 S[q] = c2(S[q].x + t1.x, S[q].y + t1.y);
             }
@@ -1036,12 +1041,12 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
 #pragma unroll
         for (int q = 0; q < 8; q++) e[0][q] = S[br3(q)];
 #ifndef TFHE_KO_INV
-        fft512<1, true>(e, s_x, T, t);
+        fft512<1, true, FU>(e, s_x, T, t);
 #endif
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             double re, im;
-            untwist_out<false>(e[0][q], twist_t[64 * q], re, im);
+            untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
             acc[q] += to_torus<SMALL>(re);
             acc[q + 8] += to_torus<SMALL>(im);
         }
@@ -1089,7 +1094,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
 constexpr int BW_WAVES = 8;
 constexpr size_t BR_WIDE_MAX_ITEMS = 512;  // measured: 1 gate 4.3 vs 9.9 ms; 512 gates 8.8 vs 10.2 ms; 1024: 17.1 vs 10.4 ms
 
-template <int L, bool SMALL>
+template <int L, bool SMALL, bool FU = false>
 __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
@@ -1169,15 +1174,15 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
                 const bool n0 = ((rb + 64 * m) & 1024) != 0, n1 = ((rb + 64 * (m + 8)) & 1024) != 0;
                 const uint32_t x0 = (n0 ? 0u - rot[m] : rot[m]) - own[m] + P.offset;
                 const uint32_t x1 = (n1 ? 0u - rot[m + 8] : rot[m + 8]) - own[m + 8] + P.offset;
-                d[0][q] = twist_in(digit_f64(x0, level, P.bgbit), digit_f64(x1, level, P.bgbit), twist_t[64 * m]);
+                d[0][q] = twist_in<FU>(digit_f64(x0, level, P.bgbit), digit_f64(x1, level, P.bgbit), twist_t[64 * m]);
             }
-            fft512<1, false>(d, s_prod[0][w], T, t);
+            fft512<1, false, FU>(d, s_prod[0][w], T, t);
             // this row's terms of fmaInFd1024 for both outputs, every frequency
             // (after this wave's exchanges in s_prod[0][w])
 #pragma unroll
             for (int q = 0; q < 8; q++) {
-                s_prod[0][w][t + 64 * q] = cmul_bk(d[0][q], kr[q][0]);
-                s_prod[1][w][t + 64 * q] = cmul_bk(d[0][q], kr[q][1]);
+                s_prod[0][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][0]);
+                s_prod[1][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][1]);
             }
             if (i + 1 < n) {  // next step's BK row, landing under the sum, inverse and forward phases
                 const double2 *nb = bkd + (size_t)(i + 1) * trgsw;
@@ -1209,12 +1214,12 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
             C2 e[1][8];
 #pragma unroll
             for (int q = 0; q < 8; q++) e[0][q] = s_prod[0][w][t + 64 * br3(q)];
-            fft512<1, true>(e, s_prod[0][w], T, t);
+            fft512<1, true, FU>(e, s_prod[0][w], T, t);
             uint32_t *pa = s_acc + w * 1024;
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 double re, im;
-                untwist_out<false>(e[0][q], twist_t[64 * q], re, im);
+                untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
                 pa[t + 64 * q] += to_torus<SMALL>(re);
                 pa[t + 64 * q + 512] += to_torus<SMALL>(im);
             }
@@ -1713,14 +1718,22 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     }
 #define BR_LAUNCH(L_, S_)                                                                                         \
     do {                                                                                                          \
-        if (wide) {                                                                                               \
-            hipLaunchKernelGGL((k_blind_rotate_wide<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,      \
+        if (wide && fused) {                                                                                      \
+            hipLaunchKernelGGL((k_blind_rotate_wide<L_, S_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,  \
                                testvec, bk2, out, out_mode, B);                                                   \
-            if (used) *used = "k_blind_rotate_wide<" #L_ "," #S_ "> (latency form)";                              \
+            if (used) *used = "k_blind_rotate_wide<" #L_ "," #S_ ",true> (latency form, fused)";                  \
+        } else if (wide) {                                                                                        \
+            hipLaunchKernelGGL((k_blind_rotate_wide<L_, S_, false>), grid, block, 0, s, P, T, ops, in_a, in_b,    \
+                               idx, testvec, bk2, out, out_mode, B);                                              \
+            if (used) *used = "k_blind_rotate_wide<" #L_ "," #S_ ",false> (latency form)";                        \
+        } else if (split && fused) {                                                                              \
+            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, \
+                               testvec, bk2, out, out_mode, B);                                                   \
+            if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ ",true> (split form, fused)";                   \
         } else if (split) {                                                                                       \
-            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,     \
-                               testvec, bk2, out, out_mode, B);                                                   \
-            if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ "> (split form)";                               \
+            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_, false>), grid, block, 0, s, P, T, ops, in_a, in_b,   \
+                               idx, testvec, bk2, out, out_mode, B);                                              \
+            if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ ",false> (split form)";                         \
         } else if (loader && fused) {                                                                             \
             hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, \
                                testvec, bk2, out, out_mode, B);                                                   \
