@@ -115,6 +115,20 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
+@pytest.mark.parametrize("loader", [1, 0])
+def test_whole_form_every_idle_slot_count(oracle, loader):
+    """Whole form at B = 1..8: the last workgroup has 3, 2, 1 or 0 idle gate slots
+    (clamped copies of the last item: they read in bounds, follow the barrier
+    schedule and store nothing).  Regression for the round-1 development fault in
+    test_blind_rotate_vs_oracle[80-3-whole]."""
+    c, k = ctx_for(oracle, "80")
+    cts = u32rand(rng(17), 8, k.p.n + 1)
+    want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
+    with c.options(br_form="whole", br_loader=loader):
+        for B in range(1, 9):
+            assert np.array_equal(c.blind_rotate_batch(cts[:B]), want[:B]), B
+
+
 @pytest.mark.parametrize("form", ["whole", "split", "wide"])
 def test_bootstrap_without_key_switch(oracle, form):
     """VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69) and the
