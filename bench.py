@@ -64,23 +64,26 @@ def algorithmic_bytes_per_gate(p) -> int:
 
 def f64_ops_per_cmux(L: int, fused: bool = False) -> int:
     """f64 VALU lane-operations (v_add/v_mul/v_fma_f64, one each) of one CMUX,
-    excluding the torus conversion.
+    the torus conversion's 4 adds per output coefficient (2N of them) included.
     Reference expression trees (fused=False; the reference's adds+muls): 2L
     forward + 2 inverse 512-point radix-2 FFTs (1,793 butterflies with a
     twiddle x 4 mul + 2 add, 2,304 x 4 add), 2L twists + 2 untwists (4 mul + 2 add
     per point, + the 1/1024 norm), 2L x 2 x 512 complex MACs (4 mul + 4 add).
-    L=3: 235,568; matched SQ_INSTS_VALU_{ADD,MUL}_F64 x 64 (profiles/r02a_pmc_blind_rotate.json).
+    L=3: 243,760 (PMC: 241,603 per CMUX per item, profiles/r02a_pmc_blind_rotate.json: the
+    kernel turns 48 products by an exact -1 into sign flips).
     Fused (the kernels' default at the L=3 / Bg=2^6 sets): a butterfly with a
     twiddle is 6 fma, a j = 0 one 2 add + 2 fma, a twist / untwist point 2 mul +
-    2 fma (norm folded), a MAC term 4 fma.  L=3: 143,376."""
+    2 fma (norm folded), a MAC term 4 fma.  L=3: 151,568 (PMC: 152,571 per CMUX
+    per item, profiles/r02c_pmc_blind_rotate.json)."""
+    conversion = 2 * 1024 * 4  # torus_from_f64_small: v - t, 2 frac, t + adj, + 1.5*2^52
     if fused:
         per_fft = 511 * 4 + 1793 * 6
-        return (2 * L + 2) * per_fft + 2 * L * 512 * 4 + 2 * 512 * 4 + 2 * L * 2 * 512 * 4
+        return (2 * L + 2) * per_fft + 2 * L * 512 * 4 + 2 * 512 * 4 + 2 * L * 2 * 512 * 4 + conversion
     fft_mul, fft_add = 1793 * 4, 1793 * 2 + 2304 * 4
     fwd, inv = 2 * L, 2
     mul = (fwd + inv) * fft_mul + fwd * 2048 + inv * (2048 + 1024) + 2 * L * 2 * 512 * 4
     add = (fwd + inv) * fft_add + fwd * 1024 + inv * 1024 + 2 * L * 2 * 512 * 4
-    return mul + add
+    return mul + add + conversion
 
 
 VALU_F64_PEAK = 256 * 4 * 16 * 2.4e9  # f64 VALU lane-ops/s: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz (78.6 TF FMA spec / 2)
