@@ -13,7 +13,7 @@ for B in [1, 8, 64, 128, 256, 512, 1024]:
     ops = np.zeros(B, np.uint8)
     row = [f"B={B:5d}"]
     for form in ["whole", "split", "wide"]:
-        os.environ["TFHE_BR_KERNEL"] = form
+        c.set_option("br_form", form)
         c.gate_batch(ops, A, Bc)
         t0 = time.perf_counter()
         for _ in range(3):
