@@ -226,6 +226,13 @@ def timed(fn, steps, warmup, world, device):
     return el, out
 
 
+def apply_opts(ctx, args):
+    """--opt NAME=VALUE -> tfhe_gpu_set_option (names: tfhe_amd.OPTIONS)."""
+    for kv in args.opt:
+        k, _, v = kv.partition("=")
+        ctx.set_option(k, v if k == "br_form" and not v.isdigit() else int(v))
+
+
 def per_rank_batch(args, rank, world):
     """(items on this rank, items over all ranks, scaling): --global-batch G splits
     G contiguously (strong scaling); else --batch per GPU (weak scaling)."""
@@ -257,6 +264,7 @@ def run_workload(args, rank, world, device):
     """Configs 3-5 of BASELINE.json (host-buffer APIs: PCIe copies included)."""
     pname = "uint4" if args.workload == "lut" else args.params
     ctx = tfhe_amd.Context(pname, device.index)
+    apply_opts(ctx, args)
     p = ctx.params
     sk = shared_secret_key(ctx, p, rank, world, device)
     if args.no_pack:
@@ -361,6 +369,7 @@ def run_single_process(args):
     device.  Host-buffer gate batches (PCIe in the timed region)."""
     n = args.gpus
     ctx = tfhe_amd.Context.multi(args.params, num_devices=n)
+    apply_opts(ctx, args)
     p = ctx.params
     t0 = time.perf_counter()
     sk, _ = ctx.keygen(42, 43)
@@ -423,6 +432,8 @@ def main():
     ap.add_argument("--single-process", action="store_true",
                     help="one process drives --gpus devices through the library's multi-device context")
     ap.add_argument("--no-pack", action="store_true", help="mixed/adder: circuit round packing off")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="tfhe_gpu_set_option before the run (A/B of kernel forms), e.g. br_loader=0, arith=1")
     ap.add_argument("--workload", default="nand", choices=["nand", "adder", "mixed", "lut", "reenc"],
                     help="nand = the headline metric (default); others: BASELINE configs 3-5")
     args = ap.parse_args()
@@ -447,6 +458,7 @@ def main():
         return
 
     ctx = tfhe_amd.Context(args.params, device.index)
+    apply_opts(ctx, args)
     p = ctx.params
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     bk = ksk = None

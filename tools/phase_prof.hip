@@ -44,14 +44,16 @@ int main(int argc, char **argv) {
         unsigned long long z[64] = {0};
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
         CK(hipEventRecord(e0));
-        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0));
+        LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
+        const char *form = argc > 2 ? argv[2] : "whole";
+        O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
+        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         unsigned long long c[64];
         CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
-        const char *form = getenv("TFHE_BR_KERNEL");
-        if (form && form[0] == 'w') {  // latency form: per wave, per phase (ticks per step per gate)
+        if (O.br_form == 3) {  // latency form: per wave, per phase (ticks per step per gate)
             const char *wn[7] = {"digits+fwd+publish", "barrier1", "mac+prefetch", "barrier2", "inverse+add", "barrier3", "tail"};
             printf("rep %d: %.3f ms (%zu gates); s_memtime ticks per step, per wave:\n", rep, ms, B);
             for (int k = 0; k < 6; k++) {
