@@ -1225,7 +1225,7 @@ int tfhe_gpu_set_option(tfhe_gpu_ctx *c, int key, int64_t v) {
     LaunchOpts &o = c->opts;
     switch (key) {
     case TFHE_OPT_BR_FORM:
-        if (v < 0 || v > 3) break;
+        if (v < 0 || v > 4) break;
         o.br_form = (int)v;
         return TFHE_OK;
     case TFHE_OPT_BR_LOADER:

@@ -52,7 +52,7 @@ struct DevTables {
 // for A/B runs and parity tests.  `used` (may be NULL) receives the name of
 // the kernel a launcher ran.
 struct LaunchOpts {
-    int br_form = 0;     // 0 auto, 1 whole, 2 split, 3 latency (wide)
+    int br_form = 0;     // 0 auto, 1 whole, 2 split, 3 latency (wide), 4 pair
     int br_loader = 1;   // whole form: 1 loader waves issue the BK DMAs, 0 the gate waves do
     int ks_form = 0;     // 0 lanes, 1 select / gather
     int ks_narrow = 0;   // basebit 2: 1 forces the 32-word x 4-wave blocks
