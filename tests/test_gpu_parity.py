@@ -112,8 +112,9 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
             assert c.last_kernels().endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
         if form.startswith("pair"):  # L = 1 (UINT4) runs the pair form in the reference's trees too
             assert c.last_kernels().startswith("k_blind_rotate_pair<") == (pname == "uint4" or form == "pair")
-        assert c.last_kernels().startswith({"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<",
-                                            "wide": "k_blind_rotate_wide<"}[form.split("-")[0]])
+        prefix = {"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<", "wide": "k_blind_rotate_wide<"}
+        if form.split("-")[0] in prefix:
+            assert c.last_kernels().startswith(prefix[form.split("-")[0]])
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 

@@ -1092,9 +1092,11 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
 //      the BK slot holds rows r and L+r, one LDS-DMA of 32 KB per level, double
 //      buffered, published by the level's block barrier;
 //   3. hands the partial its partner needs (h = 0 gives P_0,b, h = 1 gives
-//      P_1,a) through its LDS buffer (one barrier to publish, one to release),
-//      adds it to its own, inverse-transforms output polynomial h and updates
-//      acc_h.
+//      P_1,a): it writes it into the PARTNER's buffer, idle since the last
+//      level's barrier (every wave's last forward FFT is done), and after one
+//      barrier reads the partner's contribution from its own buffer, which
+//      nobody else touches until the next step; adds it to its own partial,
+//      inverse-transforms output polynomial h and updates acc_h.
 // Output h's spectrum is (sum over rows 0..L-1) + (sum over rows L..2L-1):
 // for L = 1 that is the reference's row order exactly (0 + t0 = t0, then
 // t0 + t1), so the form is exact with the reference's expression trees too;
@@ -1148,7 +1150,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
     C2 *s_twist = reinterpret_cast<C2 *>(smem + BP_LDS_BK + BP_LDS_TW);
     unsigned char *xbase = smem + BP_LDS_BK + BP_LDS_TW + BP_LDS_TWIST;
     C2 *s_x = reinterpret_cast<C2 *>(xbase + w * BP_LDS_X);
-    const C2 *s_xp = reinterpret_cast<const C2 *>(xbase + (w ^ 4) * BP_LDS_X);  // partner's buffer
+    C2 *s_xp = reinterpret_cast<C2 *>(xbase + (w ^ 4) * BP_LDS_X);  // partner's buffer
     uint32_t *s_xw = reinterpret_cast<uint32_t *>(s_x);
     uint16_t *s_at = reinterpret_cast<uint16_t *>(xbase + BP_WAVES * BP_LDS_X + gs * BP_LDS_AT);
     int *s_bt = reinterpret_cast<int *>(xbase + BP_WAVES * BP_LDS_X + BP_GATES * BP_LDS_AT);
@@ -1247,19 +1249,18 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
         C2 keep[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            s_x[t + 64 * q] = c2(h ? pa[q].x : pb[q].x, h ? pa[q].y : pb[q].y);
+            s_xp[t + 64 * q] = c2(h ? pa[q].x : pb[q].x, h ? pa[q].y : pb[q].y);
             keep[q] = c2(h ? pb[q].x : pa[q].x, h ? pb[q].y : pa[q].y);
         }
         __syncthreads();  // both partials published
         C2 e[1][8];
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            const C2 o = s_xp[t + 64 * br3(q)];
+            const C2 o = s_x[t + 64 * br3(q)];
             const C2 mine = keep[br3(q)];
             const C2 lo = c2(h ? o.x : mine.x, h ? o.y : mine.y), hi = c2(h ? mine.x : o.x, h ? mine.y : o.y);
             e[0][q] = c2(lo.x + hi.x, lo.y + hi.y);  // rows 0..L-1 first, then rows L..2L-1
         }
-        __syncthreads();  // the partner has read this wave's buffer
         fft512<1, true, FU>(e, s_x, T, t);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
