@@ -186,6 +186,10 @@ def rooflines(p, B, params, br_avg_s, kernel):
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
             "kernel": kernel, "kernel_avg_ms": round(br_avg_s * 1e3, 3),
             "algorithmic_f64_ops_per_launch": ops, "f64_ops_per_cmux": per_cmux,
+            # the reference's work (its expression trees' adds + muls) per second: what the
+            # fused kernel's fewer instructions deliver, against the same issue peak
+            "reference_equivalent": {"achieved": round(f64_ops_per_cmux(p.L) * p.n * B / br_avg_s / 1e12, 3),
+                                     "frac": round(f64_ops_per_cmux(p.L) * p.n * B / br_avg_s / VALU_F64_PEAK, 4)},
             "arithmetic": "fused multiply-add (exact-integer regime, DESIGN.md §6)" if fused else "reference expression trees",
             "reference_tree_f64_ops_per_cmux": f64_ops_per_cmux(p.L)}
     if pmc:

@@ -7,7 +7,7 @@ tagged with the kernel source hash so a later kernel change is not reported
 with these bytes.  FETCH_SIZE is doubled (MI355X_MICROARCH.md: gfx950 tallies
 128-B streaming requests at 64 B); counter KB -> bytes x 1024.
 
-    python tools/pmc_traffic.py gpurun_out/<dir> [batch] [params]
+    python tools/pmc_traffic.py gpurun_out/<dir> [batch] [params] [out.json]
 """
 import collections
 import csv
@@ -31,7 +31,7 @@ def main():
     for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
-            if "k_blind_rotate<" not in k:
+            if "k_blind_rotate" not in k:
                 continue
             name = k.split("(")[0]
             c = row["Counter_Name"]
@@ -64,7 +64,7 @@ def main():
         rec["wait_any_frac_all_waves"] = round(per["SQ_WAIT_ANY"] / per["SQ_WAVE_CYCLES"], 4)
     if "SQ_ACTIVE_INST_VALU" in per and "SQ_WAVE_CYCLES" in per:
         rec["valu_active_frac_all_waves"] = round(per["SQ_ACTIVE_INST_VALU"] / per["SQ_WAVE_CYCLES"], 4)
-    out = os.path.join(ROOT, "profiles", "pmc_blind_rotate.json")
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles", "pmc_blind_rotate.json")
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
