@@ -372,7 +372,10 @@ def run_single_process(args):
     the library broadcasts the key over RCCL itself and runs one host thread per
     device.  Host-buffer gate batches (PCIe in the timed region)."""
     n = args.gpus
-    ctx = tfhe_amd.Context.multi(args.params, num_devices=n)
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n))
+    if len(devices) != n:
+        raise SystemExit(f"bench.py: --devices lists {len(devices)} ids for --gpus {n}")
+    ctx = tfhe_amd.Context.multi(args.params, devices=devices)
     apply_opts(ctx, args)
     p = ctx.params
     t0 = time.perf_counter()
@@ -397,8 +400,8 @@ def run_single_process(args):
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: fresh encryptions of uniform random bits under a seeded key (sk 42, ck 43)",
-            "config": {"workload": f"{B} NAND gate bootstraps per step over {n} device(s) of one context "
-                                   f"(tfhe_gpu_create_multi; keygen + RCCL key broadcast {keygen_s:.1f} s, untimed)",
+            "config": {"workload": f"{B} NAND gate bootstraps per step over {n} device(s) {devices} of one context "
+                                   f"(tfhe_gpu_create_multi; keygen + key broadcast {keygen_s:.1f} s, untimed)",
                        "global_batch": B, "params": args.params, "parallelism": f"dp{n} (one process)"},
             "kernels": ctx.last_kernels(), "decrypt_check": ok}
     print(json.dumps(line), flush=True)
@@ -435,6 +438,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--single-process", action="store_true",
                     help="one process drives --gpus devices through the library's multi-device context")
+    ap.add_argument("--devices", default="",
+                    help="--single-process: device ids (default 0..N-1); a device listed twice rehearses the "
+                         "sharding on one GPU (device-to-device key copy instead of RCCL)")
     ap.add_argument("--no-pack", action="store_true", help="mixed/adder: circuit round packing off")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="tfhe_gpu_set_option before the run (A/B of kernel forms), e.g. br_loader=0, arith=1")

@@ -11,5 +11,6 @@ run mixed_nopack --workload mixed --batch 8192 --steps 3 --warmup 1 --no-pack
 run lut --workload lut --batch 4096 --steps 3 --warmup 1
 run reenc --workload reenc --batch 16384 --steps 3 --warmup 1
 run single_process --single-process --gpus 1 --steps 5 --warmup 1
+run single_process2 --single-process --gpus 2 --devices 0,0 --steps 5 --warmup 1
 timeout -k 10 300 python tools/latency.py > gpurun_out/${T}_latency.txt 2>&1 || { echo "latency failed"; exit 1; }
 cat gpurun_out/${T}_latency.txt
