@@ -256,8 +256,66 @@ DEV void exchange1(C2 (*d)[8], C2 *xb, int t) {
     wave_sync();
 }
 
+// Exchange 2 in registers, for the single-transform fft512 (latency, pair and
+// split forms, stage kernels; -DTFHE_EX2_LDS restores the LDS exchange there):
+// the latency form's 16-bit adder 114.5 -> 111.9 ms, the pair form 8.31 -> 7.99
+// ms.  The pipelined pair of the whole form (fft512_x2) keeps the LDS exchange,
+// which its other transform's butterflies hide: 7.52 vs 7.75 ms with registers
+// (profiles/r02_ab_exchange2.txt).
+// Lane t = 8a + b holds positions b + 8q + 64a (q < 8) after pass B; pass C
+// needs lane 8q + b to hold it in register a: an 8 x 8 transpose of (lane bits
+// 3-5, register bits 0-2) among the 8 lanes sharing b, done as three swap
+// rounds, one per bit pair: lane bit 5 <-> register bit 2 by
+// v_permlane32_swap, lane bit 4 <-> bit 1 by v_permlane16_swap, lane bit 3 <->
+// bit 0 by two bank-masked DPP row_ror:8 moves.  Pure data movement: the same
+// values as the LDS exchange, 80 VALU moves instead of 8 ds_write_b128 + 8
+// ds_read_b128 (a ds_write_b128 holds the CU's LDS write path ~13 cycles).
+DEV void c2_words(const C2 &v, uint32_t *w) {
+    w[0] = (uint32_t)__double2loint(v.x);
+    w[1] = (uint32_t)__double2hiint(v.x);
+    w[2] = (uint32_t)__double2loint(v.y);
+    w[3] = (uint32_t)__double2hiint(v.y);
+}
+DEV C2 c2_from_words(const uint32_t *w) {
+    return c2(__hiloint2double((int)w[1], (int)w[0]), __hiloint2double((int)w[3], (int)w[2]));
+}
+template <int ROUND>
+DEV void swap_lane_reg(C2 &x, C2 &y) {  // x: register bit clear, y: set
+    uint32_t a[4], b[4];
+    c2_words(x, a);
+    c2_words(y, b);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (ROUND == 2) {  // x's lanes 32-63 <-> y's lanes 0-31
+            const auto r = __builtin_amdgcn_permlane32_swap(a[k], b[k], false, false);
+            a[k] = r[0];
+            b[k] = r[1];
+        } else if (ROUND == 1) {  // x's odd 16-lane rows <-> y's even rows
+            const auto r = __builtin_amdgcn_permlane16_swap(a[k], b[k], false, false);
+            a[k] = r[0];
+            b[k] = r[1];
+        } else {  // lane bit 3: y's lanes with bit 3 clear <- x's (lane ^ 8); x's with bit 3 set <- old y's
+            const uint32_t old_b = b[k];
+            b[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)b[k], (int)a[k], 0x128, 0xf, 0x3, false);
+            a[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)a[k], (int)old_b, 0x128, 0xf, 0xc, false);
+        }
+    }
+    x = c2_from_words(a);
+    y = c2_from_words(b);
+}
+DEV void ex2_regs(C2 *d) {
+    swap_lane_reg<2>(d[0], d[4]); swap_lane_reg<2>(d[1], d[5]); swap_lane_reg<2>(d[2], d[6]); swap_lane_reg<2>(d[3], d[7]);
+    swap_lane_reg<1>(d[0], d[2]); swap_lane_reg<1>(d[1], d[3]); swap_lane_reg<1>(d[4], d[6]); swap_lane_reg<1>(d[5], d[7]);
+    swap_lane_reg<0>(d[0], d[1]); swap_lane_reg<0>(d[2], d[3]); swap_lane_reg<0>(d[4], d[5]); swap_lane_reg<0>(d[6], d[7]);
+}
+
 template <int NF>
 DEV void exchange2(C2 (*d)[8], C2 *xb, int t) {
+#ifndef TFHE_EX2_LDS
+#pragma unroll
+    for (int f = 0; f < NF; f++) ex2_regs(d[f]);
+    return;
+#endif
     int wb = (t & 7) + 64 * (t >> 3);
 #pragma unroll
     for (int f = 0; f < NF; f++)
@@ -317,6 +375,15 @@ DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     T.pass_b(wb_, t);
     passBC<INV, FU>(d[0], wb_);
     ex1_read(d[1], x1, t);
+#ifdef TFHE_EX2_REGS_X2  // register exchange 2 here too: 7.75 vs 7.52 ms per 1,024 gates (not kept)
+    ex2_regs(d[0]);
+    wave_sync();  // d[1]'s exchange reads precede any later write into the buffer
+    passBC<INV, FU>(d[1], wb_);
+    T.pass_c(wc_, t);
+    ex2_regs(d[1]);
+    passBC<INV, FU>(d[0], wc_);
+    passBC<INV, FU>(d[1], wc_);
+#else
     ex2_write(d[0], x0, t);
     wave_sync();
     passBC<INV, FU>(d[1], wb_);
@@ -328,6 +395,7 @@ DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     ex2_read(d[1], x1, t);
     wave_sync();
     passBC<INV, FU>(d[1], wc_);
+#endif
 }
 
 template <int NF, bool INV, bool FU = false, class TW>
