@@ -146,8 +146,19 @@ int main() {
         const CloudKey ck2 = CloudKey::loadFile(params::SECURITY_128_BIT(), path);
         const TLWELv0 x = enc(true), y = enc(false);
         expect(gates.nandGate(x, y, ck).p == gates.nandGate(x, y, ck2).p, "key file", "same NAND bits");
-        std::remove(path.c_str());
         std::printf("ok   key file save / loadFile\n");
+        // the same key on a two-shard multi-device context (one GPU listed twice): a
+        // batch split over both shards gives the single-device bits
+        const CloudKey ckm = CloudKey::loadFile(params::SECURITY_128_BIT(), path, std::vector<int>{0, 0});
+        expect(ckm.numDevices() == 2, "multi-device", "two shards");
+        std::vector<std::pair<TLWELv0, TLWELv0>> in;
+        for (int k = 0; k < 7; k++) in.push_back({enc(k & 1), enc((k >> 1) & 1)});
+        const auto one = gates.batchNand(in, ck), two = gates.batchNand(in, ckm);
+        bool same = one.size() == two.size();
+        for (size_t k = 0; same && k < one.size(); k++) same = one[k].p == two[k].p;
+        expect(same, "multi-device", "same NAND batch bits");
+        std::remove(path.c_str());
+        std::printf("ok   multi-device context (two shards) batch\n");
     }
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "PASSED", failures);
     return failures ? 1 : 0;

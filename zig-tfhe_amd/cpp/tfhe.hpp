@@ -220,6 +220,26 @@ class CloudKey {
         check(tfhe_gpu_load_cloud_key_file(ck.ctx(), path.c_str()), "CloudKey.loadFile", ck.ctx());
         return ck;
     }
+    // The same key resident on several GPUs (tfhe_gpu_create_multi): loaded on the
+    // first, broadcast over RCCL; every batch call through it is sharded over them.
+    static CloudKey loadFile(const tfhe_params &p, const std::string &path, const std::vector<int> &devices) {
+        CloudKey ck(p, devices);
+        check(tfhe_gpu_load_cloud_key_file(ck.ctx(), path.c_str()), "CloudKey.loadFile", ck.ctx());
+        return ck;
+    }
+    static std::pair<SecretKey, CloudKey> generate(const tfhe_params &p, uint64_t secret_seed, uint64_t cloud_seed,
+                                                   const std::vector<int> &devices) {
+        CloudKey ck(p, devices);
+        SecretKey sk;
+        sk.params = p;
+        sk.key_lv0.assign(p.n, 0u);
+        sk.key_lv1.assign(p.N, 0u);
+        check(tfhe_gpu_keygen(ck.ctx(), secret_seed, cloud_seed, sk.key_lv0.data(), sk.key_lv1.data(), nullptr,
+                              nullptr),
+              "CloudKey.generate", ck.ctx());
+        return {std::move(sk), std::move(ck)};
+    }
+    int numDevices() const { return tfhe_gpu_num_devices(ctx()); }
     void save(const std::string &path) const {
         check(tfhe_gpu_save_cloud_key(ctx(), path.c_str()), "CloudKey.save", ctx());
     }
@@ -233,6 +253,11 @@ class CloudKey {
     CloudKey(const tfhe_params &p, int device) : p_(p) {
         tfhe_gpu_ctx *c = nullptr;
         check(tfhe_gpu_create(&p, device, &c), "tfhe_gpu_create");
+        ctx_.reset(c);
+    }
+    CloudKey(const tfhe_params &p, const std::vector<int> &devices) : p_(p) {
+        tfhe_gpu_ctx *c = nullptr;
+        check(tfhe_gpu_create_multi(&p, (int)devices.size(), devices.data(), &c), "tfhe_gpu_create_multi");
         ctx_.reset(c);
     }
     tfhe_params p_{};
