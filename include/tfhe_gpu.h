@@ -110,7 +110,10 @@ enum {
     TFHE_OPT_CIRCUIT_PACK = 7,    /* circuit_eval round packing: 1 (default), 0 off */
     TFHE_OPT_TWIDDLES = 8,        /* cos/sin source of the FFT tables: TFHE_TWIDDLES_* (set before a key
                                      is generated: keygen transforms the key with these tables) */
-    TFHE_OPT_ARITH = 9            /* blind-rotation f64 arithmetic: TFHE_ARITH_* */
+    TFHE_OPT_ARITH = 9,           /* blind-rotation f64 arithmetic: TFHE_ARITH_* */
+    TFHE_OPT_BR_SYNC = 10         /* whole form with loader waves: 1 per-slot LDS counters (default: gate
+                                     waves wait for their data, not for each other), 0 a workgroup
+                                     barrier per BK row pair */
 };
 /* TFHE_ARITH_AUTO (default): where the exact external product is an integer
  * polynomial the f64 evaluation rounds to (the L=3 / Bg=2^6 sets: the

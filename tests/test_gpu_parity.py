@@ -94,7 +94,7 @@ def test_key_switch_vs_oracle(oracle, pname, B, form):
 
 # ---- blind rotation / bootstrap ---------------------------------------------
 @pytest.mark.parametrize("form", ["whole", "whole-noloader", "whole-reference", "whole-noloader-reference",
-                                  "split", "wide", "pair", "pair-reference"])
+                                  "whole-barrier", "whole-barrier-reference", "split", "wide", "pair", "pair-reference"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
 def test_blind_rotate_vs_oracle(oracle, pname, B, form):
     """All kernel forms (1 wave per item with or without loader waves, fused or
@@ -106,7 +106,7 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
     cts5 = u32rand(rng(16), 5, k.p.n + 1)
     want5 = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts5])
     with c.options(br_form=form.split("-")[0], br_loader=int("noloader" not in form),
-                   arith=int(form.endswith("reference"))):
+                   arith=int(form.endswith("reference")), br_sync=int("barrier" not in form)):
         assert np.array_equal(c.blind_rotate_batch(cts), want)
         if form.startswith("whole"):  # fused arithmetic only where the external product is exact (SMALL)
             assert c.last_kernels().endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
@@ -118,8 +118,8 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
-@pytest.mark.parametrize("form,loader", [("whole", 1), ("whole", 0), ("pair", 1)])
-def test_whole_form_every_idle_slot_count(oracle, form, loader):
+@pytest.mark.parametrize("form,loader,sync", [("whole", 1, 1), ("whole", 1, 0), ("whole", 0, 0), ("pair", 1, 0)])
+def test_whole_form_every_idle_slot_count(oracle, form, loader, sync):
     """Whole form at B = 1..8: the last workgroup has 3, 2, 1 or 0 idle gate slots
     (clamped copies of the last item: they read in bounds, follow the barrier
     schedule and store nothing).  Regression for the round-1 development fault in
@@ -127,7 +127,7 @@ def test_whole_form_every_idle_slot_count(oracle, form, loader):
     c, k = ctx_for(oracle, "80")
     cts = u32rand(rng(17), 8, k.p.n + 1)
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
-    with c.options(br_form=form, br_loader=loader):
+    with c.options(br_form=form, br_loader=loader, br_sync=sync):
         for B in range(1, 9):
             assert np.array_equal(c.blind_rotate_batch(cts[:B]), want[:B]), B
 

@@ -47,6 +47,7 @@ int main(int argc, char **argv) {
         LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
         const char *form = argc > 2 ? argv[2] : "whole";
         O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
+        if (argc > 3) O.br_flags = atoi(argv[3]);  // whole form: 1 slot counters, 0 barriers
         CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
@@ -70,6 +71,10 @@ int main(int argc, char **argv) {
         for (int k = 0; k < 8; k++)
             printf("  %-16s %10.1f  %5.1f%%\n", nm[k], c[k] / (double)B / P.n, 100.0 * c[k] / tot);
         printf("  total            %10.1f\n", tot / B / P.n);
+        if (O.br_flags) {  // loader waves of the slot-counter variant (one per gate wave)
+            const char *ln[3] = {"loader: DMA landing", "loader: wait gates", "loader: issue"};
+            for (int k = 0; k < 3; k++) printf("  %-22s %10.1f\n", ln[k], c[8 + k] / (double)B / P.n);
+        }
     }
     return 0;
 }

@@ -1255,6 +1255,10 @@ int tfhe_gpu_set_option(tfhe_gpu_ctx *c, int key, int64_t v) {
     case TFHE_OPT_TWIDDLES:
         if (v != TFHE_TWIDDLES_GLIBC && v != TFHE_TWIDDLES_FDLIBM) break;
         return build_tables(c, (int)v);
+    case TFHE_OPT_BR_SYNC:
+        if (v != 0 && v != 1) break;
+        o.br_flags = (int)v;
+        return TFHE_OK;
     case TFHE_OPT_ARITH:
         if (v != TFHE_ARITH_AUTO && v != TFHE_ARITH_REFERENCE) break;
         o.arith_strict = v == TFHE_ARITH_REFERENCE;
@@ -1278,6 +1282,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_CIRCUIT_PACK: *v = c->circuit_pack; break;
     case TFHE_OPT_TWIDDLES: *v = c->twiddle_source; break;
     case TFHE_OPT_ARITH: *v = o.arith_strict ? TFHE_ARITH_REFERENCE : TFHE_ARITH_AUTO; break;
+    case TFHE_OPT_BR_SYNC: *v = o.br_flags; break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;

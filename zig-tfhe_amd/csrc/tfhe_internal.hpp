@@ -54,6 +54,7 @@ struct DevTables {
 struct LaunchOpts {
     int br_form = 0;     // 0 auto, 1 whole, 2 split, 3 latency (wide), 4 pair
     int br_loader = 1;   // whole form: 1 loader waves issue the BK DMAs, 0 the gate waves do
+    int br_flags = 1;    // whole form with loader waves: 1 slot counters (default), 0 a barrier per row pair
     int ks_form = 0;     // 0 lanes, 1 select / gather
     int ks_narrow = 0;   // basebit 2: 1 forces the 32-word x 4-wave blocks
     int ks_groups = 0;   // basebit >= 5: item groups per block (0 auto = 4; 1, 2, 4, 8)

@@ -679,8 +679,59 @@ constexpr int BR_LDS_TWIST = 512 * 16;                // twist factors
 constexpr int BR_LDS_ACC = 2048 * 4;                  // per wave
 constexpr int BR_LDS_X = 512 * 16;                    // per wave, one exchange buffer for both FFTs
 constexpr int BR_LDS_AT = 1024 * 2;                   // per wave
+constexpr int BR_LDS_SYNC = 64;                      // slot counters of the flag-synchronised variant
 constexpr int BR_LDS_TOTAL =
-    BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST + BR_WAVES * (BR_LDS_ACC + BR_LDS_X + BR_LDS_AT);
+    BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST + BR_WAVES * (BR_LDS_ACC + BR_LDS_X + BR_LDS_AT) + BR_LDS_SYNC;
+
+// Flag-synchronised loader variant (FLAGS; TFHE_OPT_BR_SYNC = 1): instead of one
+// workgroup barrier per row pair, monotonic LDS counters per BK slot.  A
+// loader wave adds 1 to pub[s] once its pieces of a pair landed in slot s; a
+// gate wave reads the pair once pub[s] reached 4 x (its use of the slot + 1),
+// and adds 1 to done[s] after its MAC; a loader refills slot s once done[s]
+// shows every gate wave through the previous use.  Gate waves then wait only
+// for data, not for each other.  Every wait is bounded (BR_SPIN_CAP polls):
+// a broken protocol ends the kernel with wrong words, never a hang.
+constexpr uint32_t BR_SPIN_CAP = 1u << 22;
+DEV void spin_until_ge(const uint32_t *p, uint32_t target) {
+    // the poll loop in asm: every lane reads the same word, the loop stays
+    // scalar, and hipcc sees one instruction (a compiler-visible loop here made
+    // it hoist address arithmetic out of the step loop and spill)
+    const uint32_t addr = (uint32_t)(size_t)(const lds_void_t *)p;
+    uint32_t v, sv, cnt;
+    asm volatile(
+        "s_mov_b32 %[cnt], %[cap]\n"
+        "1:\n\t"
+        "ds_read_b32 %[v], %[addr]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readfirstlane_b32 %[sv], %[v]\n\t"
+        "s_cmp_ge_u32 %[sv], %[tgt]\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "s_sleep 1\n\t"
+        "s_sub_u32 %[cnt], %[cnt], 1\n\t"
+        "s_cmp_eq_u32 %[cnt], 0\n\t"
+        "s_cbranch_scc0 1b\n"
+        "2:"
+        : [v] "=&v"(v), [sv] "=&s"(sv), [cnt] "=&s"(cnt)
+        : [addr] "v"(addr), [tgt] "s"(target), [cap] "s"(BR_SPIN_CAP)
+        : "memory", "scc");
+}
+// One add per wave (lane 0's), without a branch: a divergent `if (lane == 0)`
+// around an atomic split the live ranges of the MAC and spilled 396 B per lane.
+// The LDS unit executes a wave's LDS instructions in order, so the add lands
+// after every LDS read the wave issued before it; a loader's DMA is waited for
+// (vmcnt) before its add.
+DEV void counter_add(uint32_t *p) {
+    const uint32_t addr = (uint32_t)(size_t)(lds_void_t *)p;
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "ds_add_u32 %[addr], %[one]\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [save] "=&s"(save)
+        : [addr] "v"(addr), [one] "v"(1u)
+        : "memory");
+}
 
 // Digits of decomposition row `row` read from the wave's LDS copy of
 // (rot - acc + offset): polynomial a at [0, 1024), b at [1024, 2048).  `row`
@@ -745,10 +796,10 @@ DEV void issue_bk_pair_async(const double2 *__restrict__ src, double2 *slot, int
     }
 }
 
-template <int L, bool LOADER, bool FU = false>
+template <int L, bool LOADER, bool FU = false, bool FLAGS = false>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
-                  PhaseProf &pp) {
+                  PhaseProf &pp, uint32_t *sync = nullptr, uint32_t k0 = 0) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
         fa[q] = c2(0.0, 0.0);
@@ -764,12 +815,18 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #endif
         pp.mark(2);
         const int slot = (slot0 + rp) & 1;
+        if (FLAGS) {  // pair k = k0 + rp is use (k >> 1) of slot k & 1: wait until all 4 loaders published it
+            const uint32_t k = k0 + (uint32_t)rp;
+            spin_until_ge(sync + (k & 1), 4u * ((k >> 1) + 1u));
+            __builtin_amdgcn_sched_barrier(0);  // as the barrier did: nothing moves across the wait
+        } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the pair's DMA landed
 #ifndef TFHE_KO_BAR
         // the pair is in slot `slot` for every wave, and every wave is done
         // with the previous pair (the other slot), which the next DMA refills
         __syncthreads();
 #endif
+        }
         pp.mark(7);
 #ifndef TFHE_KO_DMA
         if (!LOADER && (rp + 1 < L || has_next))
@@ -781,6 +838,10 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #else
         for (int q = 0; q < 8; q++) fa[q] = c2(fa[q].x + d[0][q].x, fa[q].y + d[1][q].y);
 #endif
+        if (FLAGS) {  // done with this use of the slot
+            __builtin_amdgcn_sched_barrier(0);
+            counter_add(sync + 2 + ((k0 + (uint32_t)rp) & 1));
+        }
         pp.mark(4);
     }
 }
@@ -788,7 +849,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 // LOADER: 4 more waves per workgroup, one beside each gate's wave on its SIMD,
 // issue the BK row-pair DMAs (the same pieces, slots and barriers), so the
 // gate waves only compute.
-template <int L, bool SMALL, bool LOADER = false, bool FU = false>
+template <int L, bool SMALL, bool LOADER = false, bool FU = false, bool FLAGS = false>
 __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
@@ -799,7 +860,40 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     const int t = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     double2 *s_bk = reinterpret_cast<double2 *>(smem);
-    if constexpr (LOADER) {
+    // FLAGS: pub[2], done[2] (zeroed by the gate waves before the prologue barrier)
+    uint32_t *s_sync = reinterpret_cast<uint32_t *>(smem + BR_LDS_TOTAL - BR_LDS_SYNC);
+    if constexpr (LOADER && FLAGS) {
+        if (w >= BR_WAVES) {  // loader wave, counter protocol (see spin_until_ge)
+            const int ltid = tid - 64 * BR_WAVES;
+            __builtin_amdgcn_s_setprio(3);
+            const size_t stride = (size_t)L * 2048;
+            const uint32_t pairs = (uint32_t)P.n * L;
+            issue_bk_pair_async(bkd, s_bk, ltid);  // pair 0 into slot 0
+            __syncthreads();                       // the gate waves' prologue barrier (counters zeroed)
+            PhaseProf lp;  // loader phases (TFHE_PHASE_PROF): 0 DMA landing, 1 waiting for the gates, 2 issue
+            lp.start();
+            for (uint32_t k = 0; k < pairs; k++) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of pair k landed
+                lp.mark(1);
+                counter_add(s_sync + (k & 1));
+                if (k + 1 < pairs) {
+                    const uint32_t k1 = k + 1;
+                    spin_until_ge(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1));  // every gate done with pair k1 - 2
+                    lp.mark(2);
+                    issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048,
+                                        s_bk + (k1 & 1) * 2048, ltid);
+                    lp.mark(0);
+                }
+            }
+            lp.mark(3);
+#ifdef TFHE_PHASE_PROF
+            if (ltid % 64 == 0)
+                for (int q = 0; q < 4; q++) atomicAdd(&g_phase_cycles[8 + q], (unsigned long long)lp.acc[q]);
+#endif
+            return;
+        }
+    }
+    if constexpr (LOADER && !FLAGS) {
         if (w >= BR_WAVES) {  // loader wave: one barrier per row pair, like the gate waves
             const int ltid = tid - 64 * BR_WAVES;
             // top issue priority: a loader wave's DMA issue and barrier arrival
@@ -842,6 +936,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     const size_t step_stride = (size_t)L * 2048;  // double2 per TRGSW (BK[i])
 
     if (!LOADER) issue_bk_pair(bkd, s_bk, tid);  // pair (0, 0), lands under the prologue
+    if (FLAGS && tid < 4) s_sync[tid] = 0u;
     for (int x = tid; x < 511; x += 256) s_tw[x] = TT.tw[x];
     for (int x = tid; x < 512; x += 256) s_twist[x] = TT.twist[x];
 
@@ -914,8 +1009,9 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         wave_sync();
         C2 fa[8], fb[8];
         at_next = s_at[i + 1 < n ? i + 1 : i];
-        br_pairs<L, LOADER, FU>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
-                                bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp);
+        br_pairs<L, LOADER, FU, FLAGS>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
+                                       bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp, s_sync,
+                                       (uint32_t)(L * i));
         pp.mark(5);
         inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB);
         wave_sync();
@@ -2058,6 +2154,14 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
             hipLaunchKernelGGL((k_blind_rotate_split<L_, S_, false>), grid, block, 0, s, P, T, ops, in_a, in_b,   \
                                idx, testvec, bk2, out, out_mode, B);                                              \
             if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ ",false> (split form)";                         \
+        } else if (loader && fused && O.br_flags) {                                                               \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, S_, true>), grid, block, 0, s, P, T, ops, in_a, in_b,\
+                               idx, testvec, bk2, out, out_mode, B);                                              \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true,true,true> (whole form, loader waves, slot counters, fused)"; \
+        } else if (loader && O.br_flags) {                                                                        \
+            hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, false, true>), grid, block, 0, s, P, T, ops, in_a,   \
+                               in_b, idx, testvec, bk2, out, out_mode, B);                                        \
+            if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true,false,true> (whole form, loader waves, slot counters)"; \
         } else if (loader && fused) {                                                                             \
             hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, \
                                testvec, bk2, out, out_mode, B);                                                   \
