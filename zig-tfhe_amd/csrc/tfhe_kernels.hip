@@ -692,6 +692,19 @@ constexpr int BR_LDS_TOTAL =
 // for data, not for each other.  Every wait is bounded (BR_SPIN_CAP polls):
 // a broken protocol ends the kernel with wrong words, never a hang.
 constexpr uint32_t BR_SPIN_CAP = 1u << 22;
+// The loader waves poll `done` at s_sleep 12 (~770 cycles) and normal issue
+// priority: their polls (an LDS read and a v_readfirstlane each) had taken
+// issue and LDS slots from the gate wave on the same SIMD.  A refill is due two
+// MACs (~9 k cycles) before its use, so the coarse poll never makes it late:
+// 7.39 -> 6.98 ms per 1,024 gates (sleep 1 at priority 3 before;
+// profiles/r02_ab_loader_poll.txt).
+#ifndef TFHE_LOADER_SLEEP
+#define TFHE_LOADER_SLEEP 12
+#endif
+#ifndef TFHE_LOADER_PRIO
+#define TFHE_LOADER_PRIO 0
+#endif
+template <int SLEEP = 1>
 DEV void spin_until_ge(const uint32_t *p, uint32_t target) {
     // the poll loop in asm: every lane reads the same word, the loop stays
     // scalar, and hipcc sees one instruction (a compiler-visible loop here made
@@ -706,13 +719,13 @@ DEV void spin_until_ge(const uint32_t *p, uint32_t target) {
         "v_readfirstlane_b32 %[sv], %[v]\n\t"
         "s_cmp_ge_u32 %[sv], %[tgt]\n\t"
         "s_cbranch_scc1 2f\n\t"
-        "s_sleep 1\n\t"
+        "s_sleep %[sl]\n\t"
         "s_sub_u32 %[cnt], %[cnt], 1\n\t"
         "s_cmp_eq_u32 %[cnt], 0\n\t"
         "s_cbranch_scc0 1b\n"
         "2:"
         : [v] "=&v"(v), [sv] "=&s"(sv), [cnt] "=&s"(cnt)
-        : [addr] "v"(addr), [tgt] "s"(target), [cap] "s"(BR_SPIN_CAP)
+        : [addr] "v"(addr), [tgt] "s"(target), [cap] "s"(BR_SPIN_CAP / SLEEP), [sl] "i"(SLEEP)
         : "memory", "scc");
 }
 // One add per wave (lane 0's), without a branch: a divergent `if (lane == 0)`
@@ -865,7 +878,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     if constexpr (LOADER && FLAGS) {
         if (w >= BR_WAVES) {  // loader wave, counter protocol (see spin_until_ge)
             const int ltid = tid - 64 * BR_WAVES;
-            __builtin_amdgcn_s_setprio(3);
+            __builtin_amdgcn_s_setprio(TFHE_LOADER_PRIO);
             const size_t stride = (size_t)L * 2048;
             const uint32_t pairs = (uint32_t)P.n * L;
             issue_bk_pair_async(bkd, s_bk, ltid);  // pair 0 into slot 0
@@ -878,7 +891,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
                 counter_add(s_sync + (k & 1));
                 if (k + 1 < pairs) {
                     const uint32_t k1 = k + 1;
-                    spin_until_ge(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1));  // every gate done with pair k1 - 2
+                    spin_until_ge<TFHE_LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1));  // every gate done with pair k1 - 2
                     lp.mark(2);
                     issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048,
                                         s_bk + (k1 & 1) * 2048, ltid);
