@@ -73,10 +73,12 @@ def f64_ops_per_cmux(L: int, fused: bool = False) -> int:
     kernel turns 48 products by an exact -1 into sign flips).
     Fused (the kernels' default at the L=3 / Bg=2^6 sets): a butterfly with a
     twiddle is 6 fma, a j = 0 one 2 add + 2 fma, a twist / untwist point 2 mul +
-    2 fma (norm folded), a MAC term 4 fma.  L=3: 151,568 (PMC: 152,571 per CMUX
-    per item, profiles/r02c_pmc_blind_rotate.json)."""
+    2 fma (norm folded), a MAC term 4 fma, a torus conversion 1 add.  L=3: 145,424
+    (151,568 with round 2's 4-add conversion; PMC 152,571 per CMUX per item for that
+    build, profiles/r02c_pmc_blind_rotate.json)."""
     conversion = 2 * 1024 * 4  # torus_from_f64_small: v - t, 2 frac, t + adj, + 1.5*2^52
-    if fused:
+    if fused:  # torus_from_f64_near_integer: one add (v + 1.5*2^52) per coefficient
+        conversion = 2 * 1024
         per_fft = 511 * 4 + 1793 * 6
         return (2 * L + 2) * per_fft + 2 * L * 512 * 4 + 2 * 512 * 4 + 2 * L * 2 * 512 * 4 + conversion
     fft_mul, fft_add = 1793 * 4, 1793 * 2 + 2304 * 4

@@ -405,8 +405,12 @@ void oracle_fft(uint32_t N, const double *in, uint32_t *out) {
         double f_re = buf[i].re, f_im = buf[i].im;
         double tmp_re = (g_fused ? fma(f_re, w_re, f_im * w_im) : f_re * w_re + f_im * w_im) * normalization;
         double tmp_im = (g_fused ? fma(f_im, w_re, -(f_re * w_im)) : f_im * w_re - f_re * w_im) * normalization;
-        int64_t rr = (int64_t)round(tmp_re);
-        int64_t ri = (int64_t)round(tmp_im);
+        /* reference: @round, half away from zero.  Fused mode restates the fused
+         * kernels' conversion (to_torus<SMALL, true>, tfhe_kernels.hip): round to
+         * nearest even (there, v + 1.5*2^52).  Inside the exact-integer regime the
+         * two agree: v is within ~0.1 of an integer, so no tie occurs. */
+        int64_t rr = (int64_t)(g_fused ? nearbyint(tmp_re) : round(tmp_re));
+        int64_t ri = (int64_t)(g_fused ? nearbyint(tmp_im) : round(tmp_im));
         double e_re = fabs(tmp_re - round(tmp_re)), e_im = fabs(tmp_im - round(tmp_im));
         if (e_re > tl_round_err) tl_round_err = e_re;
         if (e_im > tl_round_err) tl_round_err = e_im;

@@ -471,8 +471,20 @@ DEV uint32_t torus_from_f64_small(double v) {
     return (uint32_t)__double_as_longlong(s);
 }
 
-template <bool SMALL>
+// Fused kernels (FU, the exact-integer regime of DESIGN.md §6.1): v lies within
+// ~0.1 of the integer I the reference rounds its own value to, so every
+// rounding of v gives I and no tie can occur.  One add does it: v + 1.5*2^52
+// rounds to nearest and leaves I mod 2^32 in the low mantissa word (|v| < 2^51).
+// 1 f64 op per coefficient instead of 6 (2 trunc + 4 add).
+DEV uint32_t torus_from_f64_near_integer(double v) {
+    return (uint32_t)__double_as_longlong(v + 6755399441055744.0);
+}
+
+template <bool SMALL, bool FU = false>
 DEV uint32_t to_torus(double v) {
+#ifndef TFHE_FU_EXACT_ROUND
+    if (FU) return torus_from_f64_near_integer(v);
+#endif
     return SMALL ? torus_from_f64_small(v) : torus_from_f64(v);
 }
 
@@ -611,10 +623,10 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
         const C2 w = tws[q * TS];
         untwist_out<false, FU>(e[0][q], w, ra, ia);
         untwist_out<false, FU>(e[1][q], w, rb, ib);
-        accA[q] += to_torus<SMALL>(ra);
-        accA[q + 8] += to_torus<SMALL>(ia);
-        accB[q] += to_torus<SMALL>(rb);
-        accB[q + 8] += to_torus<SMALL>(ib);
+        accA[q] += to_torus<SMALL, FU>(ra);
+        accA[q + 8] += to_torus<SMALL, FU>(ia);
+        accB[q] += to_torus<SMALL, FU>(rb);
+        accB[q + 8] += to_torus<SMALL, FU>(ib);
     }
 }
 
@@ -1224,8 +1236,8 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
         for (int q = 0; q < 8; q++) {
             double re, im;
             untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-            acc[q] += to_torus<SMALL>(re);
-            acc[q + 8] += to_torus<SMALL>(im);
+            acc[q] += to_torus<SMALL, FU>(re);
+            acc[q + 8] += to_torus<SMALL, FU>(im);
         }
         wave_sync();
 #pragma unroll
@@ -1443,8 +1455,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
         for (int q = 0; q < 8; q++) {
             double re, im;
             untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-            acc[q] += to_torus<SMALL>(re);
-            acc[q + 8] += to_torus<SMALL>(im);
+            acc[q] += to_torus<SMALL, FU>(re);
+            acc[q + 8] += to_torus<SMALL, FU>(im);
         }
     }
 
@@ -1614,8 +1626,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
             for (int q = 0; q < 8; q++) {
                 double re, im;
                 untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-                pa[t + 64 * q] += to_torus<SMALL>(re);
-                pa[t + 64 * q + 512] += to_torus<SMALL>(im);
+                pa[t + 64 * q] += to_torus<SMALL, FU>(re);
+                pa[t + 64 * q + 512] += to_torus<SMALL, FU>(im);
             }
         }
         pp.mark(5);
