@@ -467,3 +467,25 @@ def test_options_validation_and_report(oracle):
     with c.options(arith=tfhe_amd.ARITH_REFERENCE):
         c.bootstrap_batch(cts)
         assert c.last_kernels() == "k_blind_rotate_wide<3,true,false> (latency form) + k_key_switch_lanes<9,2,32,4,1>"
+
+
+def test_slot_counters_and_barrier_agree_at_full_size(oracle):
+    """The whole form's two BK-slot protocols (LDS slot counters, the default, and a
+    workgroup barrier per row pair; TFHE_OPT_BR_SYNC) give identical words on a full
+    and a ragged headline-size batch (256 / 257 workgroups, every CU), and the NAND
+    truth table decrypts right."""
+    c, k = ctx_for(oracle, "128")
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    g = rng(95)
+    for Bn in (1024, 1027):
+        a_bits, b_bits = g.integers(0, 2, Bn).astype(np.uint8), g.integers(0, 2, Bn).astype(np.uint8)
+        A, B = sk.encrypt_bool(a_bits, seed0=95_000), sk.encrypt_bool(b_bits, seed0=96_000)
+        ops = np.zeros(Bn, np.uint8)
+        with c.options(br_form="whole", br_sync=1):
+            flags = c.gate_batch(ops, A, B)
+            assert "slot counters" in c.last_kernels()
+        with c.options(br_form="whole", br_sync=0):
+            bar = c.gate_batch(ops, A, B)
+            assert "slot counters" not in c.last_kernels()
+        assert np.array_equal(flags, bar)
+        assert np.array_equal(sk.decrypt_bool(flags), ~(a_bits.astype(bool) & b_bits.astype(bool)))
