@@ -105,7 +105,9 @@ enum {
     TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
     TFHE_OPT_KS_FORM = 3,         /* key switch: 0 lanes (default), 1 select / gather */
     TFHE_OPT_KS_NARROW = 4,       /* basebit 2: 0 auto (default), 1 32-word x 4-wave blocks */
-    TFHE_OPT_KS_ITEM_GROUPS = 5,  /* basebit >= 5: item groups per block, 0 auto (4), 1, 2, 4, 8 */
+    TFHE_OPT_KS_ITEM_GROUPS = 5,  /* basebit >= 5: 0 auto (above 64 items the ring form: 4 item groups
+                                     share a 4-deep DMA ring), 1, 2, 4, 8 forces the lane form with
+                                     that many item groups per block */
     TFHE_OPT_KS_SEL_ITEMS = 6,    /* select / gather form: items per block, 8 (default), 16, 32 */
     TFHE_OPT_CIRCUIT_PACK = 7,    /* circuit_eval round packing: 1 (default), 0 off */
     TFHE_OPT_TWIDDLES = 8,        /* cos/sin source of the FFT tables: TFHE_TWIDDLES_* (set before a key

@@ -82,7 +82,7 @@ def test_external_product_vs_oracle(oracle, pname):
 
 
 @pytest.mark.parametrize("form", ["lanes", "lanes-narrow", "sel"])
-@pytest.mark.parametrize("pname,B", [("128", 9), ("128", 130), ("80", 1), ("80", 65), ("uint4", 17)])
+@pytest.mark.parametrize("pname,B", [("128", 9), ("128", 130), ("80", 1), ("80", 65), ("uint4", 17), ("uint4", 300)])
 def test_key_switch_vs_oracle(oracle, pname, B, form):
     """All key-switch forms (lane = item in wide / narrow blocks, lane = word) bit-exact, ragged B."""
     c, k = ctx_for(oracle, pname)
@@ -347,11 +347,12 @@ def test_device_resident_api_with_torch(oracle):
     assert np.array_equal(t_o.cpu().numpy().view(np.uint32), want)
 
 
-@pytest.mark.parametrize("gw", [1, 2, 4, 8])
+@pytest.mark.parametrize("gw", [0, 1, 2, 4, 8])
 def test_lut_uint4_key_switch_item_groups(oracle, gw):
-    """UINT4 key switch with 1, 2, 4 or 8 item groups per block (TFHE_OPT_KS_ITEM_GROUPS;
-    4 is the default above 64 items): 300 LUT bootstraps, outputs identical across forms,
-    samples past the first group bit-exact vs the oracle."""
+    """UINT4 key switch: the default ring form (gw 0: 4 item groups sharing one
+    4-deep ring per block) and the lane form with 1, 2, 4 or 8 item groups per block
+    (TFHE_OPT_KS_ITEM_GROUPS): 300 LUT bootstraps, samples past the first group
+    bit-exact vs the oracle."""
     c, k = ctx_for(oracle, "uint4")
     tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (3 * x + 5) % 16)
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
@@ -359,6 +360,7 @@ def test_lut_uint4_key_switch_item_groups(oracle, gw):
     cts = sk.encrypt_lwe_message(msgs, 16, seed0=4242)
     with c.options(ks_item_groups=gw):
         out = c.bootstrap_lut_batch(cts, tv)
+        assert ("k_key_switch_ring<" in c.last_kernels()) == (gw == 0)
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (3 * msgs + 5) % 16)
     for i in (0, 63, 64, 200, 299):
         want = oracle.gate_batch(k.p, np.array([255], np.uint8), cts[i][None], cts[i][None], k.ck, testvec=tv)[0]

@@ -1910,6 +1910,116 @@ __global__ __launch_bounds__(64 * WAVES) void k_key_switch_lanes(KParams P, cons
     }
 }
 
+// Ring form for keys that stream from HBM (UINT4: 323 MB, beyond the MALL).
+// The lane form's per-wave double buffer leaves one coefficient of DMA in
+// flight, and at basebit 5 a coefficient's subtractions (~150 instructions)
+// take far less than an HBM round trip: 2.65 ms per 4,096 items, latency
+// bound.  Here the GW waves of a block (one 64-item group each) share ONE ring
+// of DEPTH buffers, since they read the same chunk of the same coefficient:
+// each wave DMAs 1/GW of a buffer's KSK slots plus its own items' a_i, and a
+// block barrier per coefficient publishes buffer i (every wave waited for its
+// own pieces) and retires buffer i - 1, which is refilled DEPTH - 1 ahead.
+// A quarter of the LDS per block lets 3 blocks share a CU, and DEPTH - 1
+// coefficients are in flight per block.  Same subtractions in the same order.
+#ifndef KS_RING_DEPTH
+#define KS_RING_DEPTH 4
+#endif
+template <int N>
+DEV void wait_vmcnt_le() {  // s_waitcnt vmcnt(N), expcnt / lgkmcnt untouched
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+template <int T, int BASEBIT, int CHUNK, int GW, int DEPTH>
+__global__ __launch_bounds__(64 * GW) void k_key_switch_ring(KParams P, const uint32_t *__restrict__ lv1,
+                                                           const uint32_t *__restrict__ ksk,
+                                                           uint32_t *__restrict__ out, size_t B, int n_in,
+                                                           int in_stride) {
+    constexpr int BASE = 1 << BASEBIT;
+    constexpr int PIECES = CHUNK / 4;
+    constexpr int SLOTS = T * PIECES * BASE;  // 16-B KSK slots per coefficient
+    static_assert(SLOTS % 64 == 0, "whole DMA instructions");
+    constexpr int NDMA = SLOTS / 64;             // LDS-DMA instructions per buffer, all waves
+    constexpr int MINE = (NDMA + GW - 1) / GW;   // per wave (+ 1 for its a_i words); when GW does not
+                                                 // divide NDMA, some waves repeat another's piece
+                                                 // (the same bytes into the same slot)
+    constexpr int BUF = SLOTS + GW * 16;      // 16-B slots per buffer: KSK slots, then GW x 64 a_i words
+    static_assert(DEPTH >= 3 && (MINE + 1) * (DEPTH - 2) < 64, "ring depth");
+    __shared__ __attribute__((aligned(16))) uint4 ring[DEPTH * BUF];
+    const int lane = threadIdx.x & 63;
+    const int gw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const size_t g_raw = (size_t)blockIdx.y * (64 * GW) + gw * 64 + lane;
+    const bool valid = g_raw < B;
+    const size_t g = valid ? g_raw : B - 1;
+    const int w0 = blockIdx.x * CHUNK;
+    const size_t rs = (size_t)P.ks_stride;
+    const size_t step_i = (size_t)BASE * T * rs;
+    uint32_t src_off[MINE];
+#pragma unroll
+    for (int cc = 0; cc < MINE; cc++) {
+        const int sl = ((cc * GW + gw) % NDMA) * 64 + lane;
+        const int k = sl % BASE, piece = (sl / BASE) % PIECES, j = sl / (BASE * PIECES);
+        src_off[cc] = (uint32_t)((BASE * j + k) * rs + w0 + 4 * piece);
+    }
+    const uint32_t ring_lds = (uint32_t)(size_t)(lds_void_t *)ring;
+    const uint32_t *a_src = lv1 + g * (size_t)in_stride;
+    auto issue = [&](int i, int slot) {
+        const uint32_t *r = ksk + (size_t)i * step_i;
+#pragma unroll
+        for (int cc = 0; cc < MINE; cc++) {
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (slot * BUF + ((cc * GW + gw) % NDMA) * 64) * 16);
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(r + src_off[cc]), "s"(dst)
+                : "memory");
+        }
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (slot * BUF + SLOTS + gw * 16) * 16);
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(a_src + i), "s"(dst)
+            : "memory");
+    };
+    const uint32_t prec = 1u << (32 - (1 + BASEBIT * T));
+    uint32_t acc[CHUNK];
+#pragma unroll
+    for (int x = 0; x < CHUNK; x++) acc[x] = 0u;
+    for (int i = 0; i < DEPTH - 1 && i < n_in; i++) issue(i, i);
+    for (int i = 0; i < n_in; i++) {
+        // this wave's pieces of buffer i landed: only buffers i+1 .. i+DEPTH-2 may still be in flight
+        if (i + DEPTH - 2 < n_in) wait_vmcnt_le<(MINE + 1) * (DEPTH - 2)>();
+        else wait_vmcnt_le<0>();
+        // every wave's pieces of buffer i landed, and every wave is done reading buffer i - 1
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (i + DEPTH - 1 < n_in) issue(i + DEPTH - 1, (i + DEPTH - 1) % DEPTH);
+        const uint4 *buf = ring + (i % DEPTH) * BUF;
+        const uint32_t a = reinterpret_cast<const uint32_t *>(buf + SLOTS + gw * 16)[lane];
+        const uint32_t pk = (a + prec) >> (32 - BASEBIT * T);  // digit j at bits BASEBIT*(T-1-j)
+#pragma unroll
+        for (int j = 0; j < T; j++) {
+            const uint32_t k = (pk >> (BASEBIT * (T - 1 - j))) & (uint32_t)(BASE - 1);
+            const uint4 *sl = buf + j * PIECES * BASE + k;
+#pragma unroll
+            for (int pc = 0; pc < PIECES; pc++) {
+                const uint4 v = sl[pc * BASE];
+                acc[4 * pc + 0] -= v.x;
+                acc[4 * pc + 1] -= v.y;
+                acc[4 * pc + 2] -= v.z;
+                acc[4 * pc + 3] -= v.w;
+            }
+        }
+    }
+    const int n1 = P.n + 1;
+    if (!valid) return;
+#pragma unroll
+    for (int x = 0; x < CHUNK; x++) {
+        const int word = w0 + x;
+        if (word < n1) out[g * n1 + word] = (word == P.n ? a_src[n_in] : 0u) + acc[x];  // acc = -(sum of rows)
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Stage kernels (parity tests and key generation); same device FFT.
 // ---------------------------------------------------------------------------
@@ -2302,7 +2412,16 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
         return true;
     }
     // UINT4 (basebit 5): the 323 MB KSK streams from HBM once per item group, so
-    // 4 groups per block share each chunk through L2 (LaunchOpts::ks_groups forces 1, 2, 4 or 8)
+    // 4 groups per block share each chunk through L2, and (default) one ring of
+    // 4 buffers per block keeps 3 coefficients in flight (k_key_switch_ring).
+    // LaunchOpts::ks_groups forces the lane form with 1, 2, 4 or 8 groups.
+    if (!O.ks_groups && basebit == 5 && B > 64 && (t_ == 3 || t_ == 2)) {
+        dim3 gr(grid.x, (unsigned)((B + 255) / 256)), br(256);
+        if (t_ == 3) hipLaunchKernelGGL((k_key_switch_ring<3, 5, KL_CHUNK, 4, KS_RING_DEPTH>), gr, br, 0, s, P, in, key, out, B, n_in, in_stride);
+        else hipLaunchKernelGGL((k_key_switch_ring<2, 5, KL_CHUNK, 4, KS_RING_DEPTH>), gr, br, 0, s, P, in, key, out, B, n_in, in_stride);
+        if (used) *used = t_ == 3 ? "k_key_switch_ring<3,5,32,4,4>" : "k_key_switch_ring<2,5,32,4,4>";
+        return true;
+    }
     const int gw = O.ks_groups ? O.ks_groups : (basebit >= 5 ? 4 : 1);
     if (gw == 8 && basebit == 5 && t_ == 3 && B > 64) {  // 16-word chunks: 8 rings fit the LDS
         dim3 g8((unsigned)((P.ks_stride + 15) / 16), (unsigned)((B + 511) / 512)), b8(512);
