@@ -830,7 +830,19 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
         fa[q] = c2(0.0, 0.0);
         fb[q] = c2(0.0, 0.0);
     }
-#pragma unroll 1
+    // unrolled with loader waves: every row's source polynomial and level are
+    // compile-time constants, so pairs (0,1) and (4,5) read their one
+    // polynomial's tmp once and the digit shifts are immediates (6.78 -> 6.67 ms
+    // per 1,024 gates, 228 VGPRs, no spills; profiles/r02_ab_pair_unroll.txt).
+    // Without loader waves the gate waves also issue the DMAs and the unrolled
+    // loop spills (143-160 VGPRs at L = 3), so that form stays rolled, as does
+    // every form under TFHE_PAIR_ROLLED (A/B builds).
+#ifdef TFHE_PAIR_ROLLED
+    constexpr int PAIR_UNROLL = 1;
+#else
+    constexpr int PAIR_UNROLL = LOADER ? L : 1;
+#endif
+#pragma unroll PAIR_UNROLL
     for (int rp = 0; rp < L; rp++) {
         C2 d[2][8];
         pp.mark(1);
