@@ -801,6 +801,29 @@ DEV void load_digits_pair_lds(C2 (*d)[8], const uint32_t *s_tmp, int row, int L,
     }
 }
 
+// Digits of rows (0, 1) from the tmp words still in registers after the
+// rotation gather (lane word m = coefficient t + 64m), the same values
+// load_digits_pair_lds reads back from LDS: the first pair's transforms then
+// do not wait for an LDS round trip at the top of the step (128-bit: 6.64 ->
+// 6.60 ms per 1,024 gates; UINT4, where tB must stay live too: 1.4 % slower,
+// not used there; profiles/r02_ab_pair0_regs.txt).
+template <bool FU = false>
+DEV void load_digits_pair0_regs(C2 (*d)[8], const uint32_t *tA, const uint32_t *tB, int L, int bgbit,
+                                const C2 *twist_t) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int m = br3(q);
+        const C2 w = twist_t[64 * m];
+#pragma unroll
+        for (int f = 0; f < 2; f++) {
+            const bool from_a = f < L;
+            const uint32_t *src = from_a ? tA : tB;
+            const int level = from_a ? f : f - L;
+            d[f][q] = twist_in<FU>(digit_f64(src[m], level, bgbit), digit_f64(src[m + 8], level, bgbit), w);
+        }
+    }
+}
+
 // Row pairs of one CMUX step: forward FFTs of rows (2rp, 2rp+1), wait for the
 // pair's BK rows in LDS, MAC, release the buffer and prefetch the next pair.
 // LDS-DMA of one BK row pair (32 KB) into a slot, 8 x 16 B per thread, in
@@ -824,7 +847,8 @@ DEV void issue_bk_pair_async(const double2 *__restrict__ src, double2 *slot, int
 template <int L, bool LOADER, bool FU = false, bool FLAGS = false>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
-                  PhaseProf &pp, uint32_t *sync = nullptr, uint32_t k0 = 0) {
+                  PhaseProf &pp, uint32_t *sync = nullptr, uint32_t k0 = 0, const uint32_t *tA = nullptr,
+                  const uint32_t *tB = nullptr) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
         fa[q] = c2(0.0, 0.0);
@@ -846,7 +870,12 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
     for (int rp = 0; rp < L; rp++) {
         C2 d[2][8];
         pp.mark(1);
-        load_digits_pair_lds<FU>(d, s_tmp, 2 * rp, L, bgbit, twist_t, t);
+#ifndef TFHE_PAIR0_LDS
+        if (PAIR_UNROLL == L && LOADER && L > 1 && rp == 0)  // UINT4 (L = 1): 1.4 % slower, LDS kept
+            load_digits_pair0_regs<FU>(d, tA, tB, L, bgbit, twist_t);
+        else
+#endif
+            load_digits_pair_lds<FU>(d, s_tmp, 2 * rp, L, bgbit, twist_t, t);
 #ifndef TFHE_KO_FFT  // TFHE_KO_*: development knock-out builds (timing only)
         fft512_x2<false, true, FU>(d, xb, T, t);
 #endif
@@ -1048,7 +1077,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         at_next = s_at[i + 1 < n ? i + 1 : i];
         br_pairs<L, LOADER, FU, FLAGS>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
                                        bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp, s_sync,
-                                       (uint32_t)(L * i));
+                                       (uint32_t)(L * i), tA, tB);
         pp.mark(5);
         inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB);
         wave_sync();
