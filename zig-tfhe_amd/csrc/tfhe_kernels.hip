@@ -807,13 +807,14 @@ DEV void load_digits_pair_lds(C2 (*d)[8], const uint32_t *s_tmp, int row, int L,
 // do not wait for an LDS round trip at the top of the step (128-bit: 6.64 ->
 // 6.60 ms per 1,024 gates; UINT4, where tB must stay live too: 1.4 % slower,
 // not used there; profiles/r02_ab_pair0_regs.txt).
+// tw0[q] = twist factor of coefficient t + 64 br3(q), read with the gather.
 template <bool FU = false>
 DEV void load_digits_pair0_regs(C2 (*d)[8], const uint32_t *tA, const uint32_t *tB, int L, int bgbit,
-                                const C2 *twist_t) {
+                                const C2 *tw0) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         const int m = br3(q);
-        const C2 w = twist_t[64 * m];
+        const C2 w = tw0[q];
 #pragma unroll
         for (int f = 0; f < 2; f++) {
             const bool from_a = f < L;
@@ -848,7 +849,7 @@ template <int L, bool LOADER, bool FU = false, bool FLAGS = false>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
                   PhaseProf &pp, uint32_t *sync = nullptr, uint32_t k0 = 0, const uint32_t *tA = nullptr,
-                  const uint32_t *tB = nullptr) {
+                  const uint32_t *tB = nullptr, const C2 *tw0 = nullptr) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
         fa[q] = c2(0.0, 0.0);
@@ -872,7 +873,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
         pp.mark(1);
 #ifndef TFHE_PAIR0_LDS
         if (PAIR_UNROLL == L && LOADER && L > 1 && rp == 0)  // UINT4 (L = 1): 1.4 % slower, LDS kept
-            load_digits_pair0_regs<FU>(d, tA, tB, L, bgbit, twist_t);
+            load_digits_pair0_regs<FU>(d, tA, tB, L, bgbit, tw0);
         else
 #endif
             load_digits_pair_lds<FU>(d, s_tmp, 2 * rp, L, bgbit, twist_t, t);
@@ -1042,6 +1043,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         // tmp = X^{a~} acc - acc (+ decomposition offset), written over the
         // accumulator's LDS copy (the old acc stays in accA/accB registers)
         uint32_t tA[16], tB[16];
+        C2 tw0[8];
 #ifndef TFHE_KO_TMP
         // all 32 gathers first (one wait), then the arithmetic: interleaved,
         // hipcc waits for every gather before issuing the next
@@ -1051,6 +1053,13 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
             const int j = (rb + 64 * m) & 1023;
             tA[m] = s_acc[j];
             tB[m] = s_acc[1024 + j];
+        }
+        // pair 0's twist factors ride with the gather (one wait for both);
+        // read after the tmp stores they queued behind them (6.64 -> 6.61 ms,
+        // profiles/r02_ab_twist_preload.txt)
+        if constexpr (LOADER && L > 1) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) tw0[q] = twist_t[64 * br3(q)];
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1077,7 +1086,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         at_next = s_at[i + 1 < n ? i + 1 : i];
         br_pairs<L, LOADER, FU, FLAGS>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
                                        bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp, s_sync,
-                                       (uint32_t)(L * i), tA, tB);
+                                       (uint32_t)(L * i), tA, tB, tw0);
         pp.mark(5);
         inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB);
         wave_sync();
