@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 2
+#define TFHE_GPU_ABI_VERSION 3
 
 enum {
     TFHE_OK = 0,
@@ -37,7 +37,11 @@ enum {
     TFHE_ERR_HIP = -2,         /* HIP runtime error (no device, launch failure) */
     TFHE_ERR_NO_KEY = -3,      /* bootstrap requested before a cloud key loaded */
     TFHE_ERR_OOM = -4,         /* device allocation failed                      */
-    TFHE_ERR_IO = -5           /* key file cannot be opened, read or written    */
+    TFHE_ERR_IO = -5,          /* key file cannot be opened, read or written    */
+    TFHE_ERR_DEVICE = -6       /* a kernel reported a failure through the context's device
+                                  error word (the blind rotation's BK-slot protocol: a wait
+                                  timed out); the outputs since the last synchronisation are
+                                  invalid; the word is cleared and the context stays usable */
 };
 
 /* Gate op codes — gates.zig:48-121 (pre-combination constants SURVEY §8a A2). */
@@ -68,11 +72,23 @@ typedef struct {
 typedef struct tfhe_gpu_ctx tfhe_gpu_ctx;
 
 int         tfhe_gpu_abi_version(void);
-/* Context on HIP device `device`.  Replaces the implicit per-thread FFT plan
- * (fft.zig:983-992) and owns the device copy of the CloudKey. */
-int         tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out);
+/* 16 hex digits of the sha256 of the kernels object this library was linked
+ * from (its gfx950 code): measurements (PMC records) are tagged with it. */
+const char *tfhe_gpu_build_id(void);
+/* Context over HIP devices 0..num_devices-1 of this node:
+ * num_devices = 1 is a plain single-device context on device 0, more is the
+ * multi-device context of tfhe_gpu_create_multi below.  Replaces the implicit
+ * per-thread FFT plan (fft.zig:983-992) and owns the device copy of the
+ * CloudKey.  TFHE_ERR_HIP if the node has fewer devices. */
+int         tfhe_gpu_create(const tfhe_params *params, int num_devices, tfhe_gpu_ctx **out);
+/* Context on the one HIP device `device` (ABI 2's tfhe_gpu_create). */
+int         tfhe_gpu_create_on_device(const tfhe_params *params, int device, tfhe_gpu_ctx **out);
 void        tfhe_gpu_destroy(tfhe_gpu_ctx *ctx);
 const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *ctx);
+/* Wait for the context's work; TFHE_ERR_DEVICE if a kernel set the device
+ * error word since the last synchronisation.  Every host-buffer entry point
+ * performs the same check before it returns; after the asynchronous _dev
+ * entry points, this (or tfhe_gpu_profile_end) is where a failure surfaces. */
 int         tfhe_gpu_sync(tfhe_gpu_ctx *ctx);
 /* Run this context's work on a caller-owned hipStream_t (NULL = own stream).
  * Multi-device context: the stream of its first device. */
@@ -90,12 +106,18 @@ int         tfhe_gpu_set_stream(tfhe_gpu_ctx *ctx, void *hip_stream);
  * the batch into contiguous slices of ceil(B/num_devices) items, one per
  * device, run them concurrently (one host thread and one stream per device)
  * and copy each slice's results into the caller's buffer; circuit_eval
- * places the connected components of the gate DAG on the devices (largest
- * first, least-loaded device), so no wire crosses a device.  Device-pointer
+ * replicates the primary inputs to every device that reads them and places
+ * the connected components of the gate DAG (gates joined by gate-to-gate
+ * wires) on the devices, largest first onto the least-loaded device, so no
+ * gate output crosses a device.  Device-pointer
  * (_dev) and stage entry points and the profile timers use the first device.
  * Nothing is exchanged between devices after the key broadcast. */
 int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int *devices, tfhe_gpu_ctx **out);
 int tfhe_gpu_num_devices(const tfhe_gpu_ctx *ctx);
+/* Blind rotations each device of the context has launched since it was
+ * created (counts[d] for device d < max_devices, in create order); returns the
+ * number of devices.  Shows where a sharded batch or circuit ran. */
+int tfhe_gpu_device_bootstraps(const tfhe_gpu_ctx *ctx, uint64_t *counts, int max_devices);
 
 /* ---- Options (kernel forms and table sources; default = the measured-
  * fastest forms).  Set on a context before use; a multi-device context
@@ -113,9 +135,12 @@ enum {
     TFHE_OPT_TWIDDLES = 8,        /* cos/sin source of the FFT tables: TFHE_TWIDDLES_* (set before a key
                                      is generated: keygen transforms the key with these tables) */
     TFHE_OPT_ARITH = 9,           /* blind-rotation f64 arithmetic: TFHE_ARITH_* */
-    TFHE_OPT_BR_SYNC = 10         /* whole form with loader waves: 1 per-slot LDS counters (default: gate
+    TFHE_OPT_BR_SYNC = 10,        /* whole form with loader waves: 1 per-slot LDS counters (default: gate
                                      waves wait for their data, not for each other), 0 a workgroup
                                      barrier per BK row pair */
+    TFHE_OPT_BR_SPIN_CAP = 11     /* polls before one slot-counter wait gives up and sets the device
+                                     error word (0 = default, 2^22 sleep units; fault-injection tests
+                                     set a few polls to see TFHE_ERR_DEVICE come back) */
 };
 /* TFHE_ARITH_AUTO (default): where the exact external product is an integer
  * polynomial the f64 evaluation rounds to (the L=3 / Bg=2^6 sets: the
@@ -229,6 +254,12 @@ int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *in
  * the MI355X), with round packing when pack != 0. */
 int tfhe_circuit_schedule(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
                           const uint32_t *in_b, uint32_t cus, int pack, uint32_t *levels, uint32_t *depth);
+
+/* The device placement a multi-device tfhe_gpu_circuit_eval uses, host only:
+ * device_of_gate[g] < num_devices.  Gates joined by gate-to-gate wires share a
+ * device; primary inputs are replicated and join nothing. */
+int tfhe_circuit_partition(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
+                           const uint32_t *in_b, int num_devices, uint32_t *device_of_gate);
 
 /* ---- Proxy re-encryption (proxy_reenc.zig) -------------
  * reencryptTLWELv0 is the identity key switch over a TLWELv0 input (n

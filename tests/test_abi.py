@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 2
+    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 3
 
 
 def test_library_is_gfx950_code_object():
@@ -46,7 +46,19 @@ def test_create_rejects_unsupported_params():
     p = tfhe_amd.make_params("128")
     p.N = 512  # only N=1024 exists in params.zig
     h = C.c_void_p()
+    assert lib.tfhe_gpu_create(C.byref(p), 1, C.byref(h)) == -1
+    assert lib.tfhe_gpu_create_on_device(C.byref(p), 0, C.byref(h)) == -1
+    assert not h.value
+
+
+def test_create_takes_a_device_count():
+    """the second argument of tfhe_gpu_create is a device COUNT
+    (devices 0..n-1), not a device id; < 1 is invalid before any device is touched."""
+    lib = tfhe_amd.load_library()
+    p = tfhe_amd.make_params("128")
+    h = C.c_void_p()
     assert lib.tfhe_gpu_create(C.byref(p), 0, C.byref(h)) == -1
+    assert lib.tfhe_gpu_create(C.byref(p), -3, C.byref(h)) == -1
     assert not h.value
 
 
@@ -119,3 +131,36 @@ def test_gates_host_only_ops():
     g.ctx = _Ctx()
     assert g.constant(True)[-1] == 0x20000000
     assert g.constant(False)[-1] == 0xE0000001
+
+
+@pytest.mark.gpu
+def test_create_one_device_through_survey_signature(oracle):
+    """tfhe_gpu_create(params, 1, &ctx) (a device count) is a context
+    on device 0; its gates are bit-exact vs the oracle."""
+    from conftest import get_keys
+    k = get_keys(oracle, "80")
+    lib = tfhe_amd.load_library()
+    h = C.c_void_p()
+    assert lib.tfhe_gpu_create(C.byref(tfhe_amd.make_params("80")), 1, C.byref(h)) == 0 and h.value
+    try:
+        assert lib.tfhe_gpu_num_devices(h) == 1
+        ck = k.ck
+        tv = np.ascontiguousarray(ck.testvec, np.uint32)
+        bk = np.ascontiguousarray(ck.bk, np.float64)
+        ksk = np.ascontiguousarray(ck.ksk, np.uint32)
+        u32p, f64p = C.POINTER(C.c_uint32), C.POINTER(C.c_double)
+        assert lib.tfhe_gpu_load_cloud_key(h, ck.offset, tv[:1024].ctypes.data_as(u32p),
+                                           tv[1024:].ctypes.data_as(u32p), bk.ctypes.data_as(f64p), bk.size,
+                                           ksk.ctypes.data_as(u32p), ksk.size) == 0
+        g = np.random.default_rng(31)
+        ops = np.arange(10, dtype=np.uint8)
+        A = g.integers(0, 1 << 32, (10, k.p.n + 1), dtype=np.uint64).astype(np.uint32)
+        B = g.integers(0, 1 << 32, (10, k.p.n + 1), dtype=np.uint64).astype(np.uint32)
+        out = np.zeros_like(A)
+        assert lib.tfhe_gpu_gate_batch(h, ops.ctypes.data_as(C.POINTER(C.c_uint8)), A.ctypes.data_as(u32p),
+                                       B.ctypes.data_as(u32p), out.ctypes.data_as(u32p), 10) == 0
+        assert np.array_equal(out, oracle.gate_batch(k.p, ops, A, B, ck, threads=8))
+        counts = (C.c_uint64 * 1)()
+        assert lib.tfhe_gpu_device_bootstraps(h, counts, 1) == 1 and counts[0] == 10
+    finally:
+        lib.tfhe_gpu_destroy(h)

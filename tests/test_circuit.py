@@ -243,10 +243,17 @@ def test_circuit_mixed_config4_128bit(oracle):
     for i in sample:
         assert np.array_equal(got[i], oracle_cone(oracle, k, c, inputs, c.outputs[i], memo)), i
     ctx.close()
+    # two shards (one GPU listed twice): the 96 shared inputs are replicated, so the
+    # gates split evenly; both shards run, the words are the single device's
     multi = tfhe_amd.Context.multi("128", devices=[0, 0])
     multi.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    before = multi.device_bootstraps()
     got2, depth2 = c.run(multi, inputs)
+    ran = multi.device_bootstraps() - before
     assert depth2 == 2 and np.array_equal(got2, got)
+    n_boot = sum(op != tfhe_amd.NOT for op in c.ops)
+    assert int(ran.sum()) == n_boot and ran.min() > 0
+    assert abs(int(ran[0]) - int(ran[1])) <= 3  # components of at most 3 bootstraps (a MUX)
     multi.close()
 
 
@@ -336,3 +343,73 @@ def test_circuit_schedule_rejects_bad_graphs_host():
         c.schedule()
     with pytest.raises(tfhe_amd.TfheError):
         Circuit().schedule(cus=0)
+
+
+def config4_circuit(n_gates, n_inputs, seed):
+    """Config 4 as bench.py --workload mixed builds it, with shared inputs: op
+    uniform over AND/OR/XOR/MUX, operands drawn from n_inputs input wires."""
+    g = np.random.default_rng(seed)
+    c = Circuit()
+    ins = [c.input() for _ in range(n_inputs)]
+    bits = g.integers(0, 2, n_inputs).astype(np.uint8)
+    kinds = g.integers(0, 4, n_gates)
+    xyz = g.integers(0, n_inputs, (n_gates, 3))
+    want = np.empty(n_gates, bool)
+    for i, (kd, (x, y, z)) in enumerate(zip(kinds, xyz)):
+        if kd == 0: c.output(c.and_(ins[x], ins[y])); want[i] = bits[x] & bits[y]
+        elif kd == 1: c.output(c.or_(ins[x], ins[y])); want[i] = bits[x] | bits[y]
+        elif kd == 2: c.output(c.xor(ins[x], ins[y])); want[i] = bits[x] ^ bits[y]
+        else: c.output(c.mux(ins[x], ins[y], ins[z])); want[i] = bits[y] if bits[x] else bits[z]
+    return c, bits, want, kinds
+
+
+def test_circuit_partition_config4_host():
+    """tfhe_circuit_partition (host only): an 8,192-gate config-4 circuit over 64
+    shared inputs splits within 1 % over 2 and over 8 devices (inputs are
+    replicated, so only a MUX's three gates stay together); one 16-bit adder is a
+    single component and stays on one device."""
+    c, _, _, _ = config4_circuit(8192, 64, 4)
+    boot = np.array([op != tfhe_amd.NOT for op in c.ops])
+    total = int(boot.sum())
+    for D in (2, 8):
+        dev = c.partition(D)
+        per = np.bincount(dev[boot], minlength=D)
+        assert per.sum() == total and (np.abs(per - total / D) <= 0.01 * total / D).all(), per
+        # every gate sits with the gates that drive it
+        for g, (op, a, b) in enumerate(zip(c.ops, c.ia, c.ib)):
+            for w in (a, b) if op != tfhe_amd.NOT else (a,):
+                if w >= c.n_inputs:
+                    assert dev[w - c.n_inputs] == dev[g]
+    a = Circuit()
+    A, B = [a.input() for _ in range(16)], [a.input() for _ in range(16)]
+    s, _ = a.ripple_add(A, B, a.input())
+    a.output(*s)
+    assert len(set(a.partition(8).tolist())) == 1
+
+
+@pytest.mark.gpu
+def test_circuit_config4_full_65536_128bit(oracle):
+    """BASELINE config 4 at its full size on one GPU: 65,536 gates, op uniform over
+    AND/OR/XOR/MUX over 64 shared inputs, 128-bit (~82 k level-1 bootstraps = 80
+    whole-form rounds, 16 k level-2 ORs).  Every gate's truth table, and an oracle
+    cone sample across level-1 rounds and MUX outputs bit-exact vs the reference's
+    gate-by-gate evaluation."""
+    from conftest import get_keys
+    k = get_keys(oracle, "128")
+    ctx = tfhe_amd.Context("128", 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    sk = tfhe_amd.SecretKey(ctx.params, k.k0, k.k1)
+    c, bits, want, kinds = config4_circuit(65536, 64, 65536)
+    inputs = sk.encrypt_bool(bits, seed0=65536)
+    before = ctx.device_bootstraps()
+    got, depth = c.run(ctx, inputs)
+    assert depth == 2
+    assert int((ctx.device_bootstraps() - before)[0]) == sum(op != tfhe_amd.NOT for op in c.ops)
+    assert np.array_equal(sk.decrypt_bool(got), want)
+    mux = np.flatnonzero(kinds == 3)
+    single = np.flatnonzero(kinds != 3)
+    sample = sorted(set(single[[0, 1, 1500, 20000, 40000, -1]].tolist() + mux[[0, 7000, -1]].tolist()))
+    memo = {}
+    for i in sample:
+        assert np.array_equal(got[i], oracle_cone(oracle, k, c, inputs, c.outputs[i], memo)), i
+    ctx.close()

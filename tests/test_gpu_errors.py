@@ -86,3 +86,45 @@ def test_refused_calls_leave_the_context_usable(oracle):
         assert np.array_equal(got, want)
     finally:
         ctx.close()
+
+
+def test_slot_protocol_failure_is_reported_not_returned(oracle):
+    """The whole form's slot-counter waits are bounded (tfhe_kernels.hip
+    spin_until_ge).  A wait that gives up must fail the call, never hand back
+    the words of a broken launch as TFHE_OK: with the bound forced down to one
+    poll (TFHE_OPT_BR_SPIN_CAP = 1; a loader waits ~24 k cycles per step for
+    the gates) the gate batch returns TFHE_ERR_DEVICE, the device error word is
+    cleared, and with the default bound the same context is bit-exact again."""
+    k = get_keys(oracle, "128")
+    p = k.p
+    ctx = tfhe_amd.Context("128", 0)
+    try:
+        ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+        ctx.set_option("br_form", "whole")  # the slot-counter form at any batch size
+        assert ctx.get_option("br_sync") == 1 and ctx.get_option("br_loader") == 1
+        a, b = _inputs(p, 8, 11), _inputs(p, 8, 12)
+        ops = np.zeros(8, np.uint8)
+        with ctx.options(br_spin_cap=1):
+            with pytest.raises(tfhe_amd.TfheError) as e:
+                ctx.gate_batch(ops, a, b)
+            assert e.value.status == tfhe_amd.ERR_DEVICE
+            assert "slot-counter protocol failure" in str(e.value)
+            # the device-pointer path surfaces it at the next synchronisation
+            import torch
+            dev = torch.device("cuda", 0)
+            t_ops = torch.zeros(8, dtype=torch.uint8, device=dev)
+            t_a = torch.from_numpy(a.view(np.int32)).to(dev)
+            t_b = torch.from_numpy(b.view(np.int32)).to(dev)
+            t_o = torch.zeros_like(t_a)
+            torch.cuda.synchronize(dev)
+            ctx.gate_batch_dev(t_ops.data_ptr(), t_a.data_ptr(), t_b.data_ptr(), t_o.data_ptr(), 8)
+            with pytest.raises(tfhe_amd.TfheError) as e:
+                ctx.sync()
+            assert e.value.status == tfhe_amd.ERR_DEVICE
+        assert ctx.get_option("br_spin_cap") == 0
+        ctx.sync()  # cleared: nothing pending
+        got = ctx.gate_batch(ops, a, b)
+        want = oracle.gate_batch(p, ops, a, b, k.ck, threads=8)
+        assert np.array_equal(got, want)
+    finally:
+        ctx.close()

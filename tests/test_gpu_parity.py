@@ -280,6 +280,27 @@ def test_lut_pbs_uint4(oracle):
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (msgs + 1) % 16)
 
 
+def test_lut_config5_full_4096_uint4(oracle):
+    """BASELINE config 5 at its full size on one GPU: 4,096 UINT4 programmable
+    bootstraps of f(x) = x^2 + 3 mod 16 (bench.py --workload lut).  Every item
+    decrypts to f(m); samples in the first and the last blocks of the ring-form
+    key switch (256 items each) and across the blind rotation's 1,024-item rounds
+    bit-exact vs the oracle."""
+    c, k = ctx_for(oracle, "uint4")
+    m = 16
+    tv = tfhe_amd.lut_generate(c.params, m, lambda x: (x * x + 3) % m)
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    msgs = rng(4096).integers(0, m, 4096).astype(np.uint32)
+    cts = sk.encrypt_lwe_message(msgs, m, seed0=40960)
+    out = c.bootstrap_lut_batch(cts, tv)
+    assert "k_key_switch_ring<" in c.last_kernels()
+    assert np.array_equal(sk.decrypt_lwe_message(out, m), (msgs * msgs + 3) % m)
+    idx = [0, 1, 255, 1023, 1024, 2047, 3071, 3840, 4000, 4095]
+    want = oracle.gate_batch(k.p, np.full(len(idx), 255, np.uint8), cts[idx], cts[idx], k.ck, testvec=tv,
+                             threads=len(idx))
+    assert np.array_equal(out[idx], want)
+
+
 def test_lut_uint4_golden_fixture(oracle):
     """The committed config-5 fixture (tests/golden/lut_uint4.npz) through
     tfhe_gpu_bootstrap_lut_batch with the oracle's seeded UINT4 key: bit-identical."""

@@ -3,8 +3,8 @@
 Reads gpurun_out/<dir>/p*/run_counter_collection.csv (one counter group per
 pass, tools/pmc_br.sh), keeps the blind-rotation launches, and writes the
 per-launch figures bench.py reports as roofline.traffic / roofline.pmc,
-tagged with the kernel source hash so a later kernel change is not reported
-with these bytes.  FETCH_SIZE is doubled (MI355X_MICROARCH.md: gfx950 tallies
+tagged with the library's kernel build id (tfhe_gpu_build_id) so a later
+kernel binary is not reported with these bytes.  FETCH_SIZE is doubled (MI355X_MICROARCH.md: gfx950 tallies
 128-B streaming requests at 64 B); counter KB -> bytes x 1024.
 
     python tools/pmc_traffic.py gpurun_out/<dir> [batch] [params] [out.json]
@@ -42,9 +42,10 @@ def main():
     per = {c: tot[c] / max(1, len(launches[c])) for c in tot}
     fetch = per.get("FETCH_SIZE", 0.0) * 1024 * 2
     write = per.get("WRITE_SIZE", 0.0) * 1024
-    import bench  # noqa: E402  (kernel_source_hash)
+    import bench  # noqa: E402  (kernel_source_hash, kernel_build_id)
     rec = {
         "kernel": name, "batch": batch, "params": params,
+        "kernel_build_id": bench.kernel_build_id(),
         "kernel_source_sha256": bench.kernel_source_hash(),
         "launches_per_pass": max(len(v) for v in launches.values()),
         "hbm_bytes_per_launch": int(fetch + write) if "FETCH_SIZE" in per and "WRITE_SIZE" in per else None,

@@ -252,7 +252,7 @@ class CloudKey {
     };
     CloudKey(const tfhe_params &p, int device) : p_(p) {
         tfhe_gpu_ctx *c = nullptr;
-        check(tfhe_gpu_create(&p, device, &c), "tfhe_gpu_create");
+        check(tfhe_gpu_create_on_device(&p, device, &c), "tfhe_gpu_create_on_device");
         ctx_.reset(c);
     }
     CloudKey(const tfhe_params &p, const std::vector<int> &devices) : p_(p) {
@@ -270,7 +270,7 @@ class HipReencryptor {
   public:
     HipReencryptor(const tfhe_params &p, const ProxyReencryptionKey &k, int device = 0) : p_(p) {
         tfhe_gpu_ctx *c = nullptr;
-        check(tfhe_gpu_create(&p, device, &c), "tfhe_gpu_create");
+        check(tfhe_gpu_create_on_device(&p, device, &c), "tfhe_gpu_create_on_device");
         ctx_.reset(c);
         tfhe_gpu_reenc_key *h = nullptr;
         check(tfhe_gpu_reenc_key_load(c, k.key_encryptions.data(), k.key_encryptions.size(), k.basebit, k.t, &h),

@@ -33,6 +33,11 @@ struct tfhe_gpu_ctx {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     std::string err;
+    // device error word (KParams::err; DEV_ERR_* bits) and its pinned host copy,
+    // read at every synchronisation point (sync_check); words 2-3 of both hold
+    // a key fingerprint (key_fingerprint)
+    uint32_t *d_err = nullptr;
+    uint32_t *h_err = nullptr;
     // constant tables
     C2 *d_twist = nullptr, *d_tw = nullptr;
     C2 twa[4] = {};  // host copy of the pass-A twiddles (DevTables::twa)
@@ -55,6 +60,7 @@ struct tfhe_gpu_ctx {
     LaunchOpts opts{};
     int64_t circuit_pack = 1;
     int64_t twiddle_source = TFHE_TWIDDLES_GLIBC;
+    bool key_from_keygen = false;  // the resident BK was transformed with this context's tables
     const char *last_br = "", *last_ks = "";
     std::string last_kernels;
     // multi-device context (tfhe_gpu_create_multi): shards[0] is this context
@@ -62,6 +68,8 @@ struct tfhe_gpu_ctx {
     // Empty for a single-device context.
     std::vector<tfhe_gpu_ctx *> shards;
     bool distinct_devices = true;    // RCCL needs each device once; else D2D copies
+    // blind rotations launched on this device since creation (tfhe_gpu_device_bootstraps)
+    uint64_t bootstraps = 0;
     std::vector<ncclComm_t> comms;   // one communicator per shard, created on the first key broadcast
 };
 
@@ -184,6 +192,7 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
     }
     HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, idx, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
                                   lv1, out_mode, B, c->stream, c->opts, &c->last_br));
+    c->bootstraps += B;
     if (ev[1]) HIPCHK(c, hipEventRecord(ev[1], c->stream));
     c->last_ks = "";
     if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream, c->opts, &c->last_ks));
@@ -198,10 +207,47 @@ int h2d(tfhe_gpu_ctx *c, DevBuf &buf, const void *src, size_t bytes) {
     return TFHE_OK;
 }
 
+// Synchronise the context stream and fail the call if a kernel on it set the
+// device error word (a slot-counter wait of the blind rotation gave up: its
+// words are not the reference's).  The word is copied into pinned host memory
+// on the stream, so the one synchronisation covers both; a reported error is
+// cleared, and the context stays usable.
+int sync_check(tfhe_gpu_ctx *c) {
+    HIPCHK(c, hipMemcpyAsync(c->h_err, c->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint32_t e = *c->h_err;
+    if (!e) return TFHE_OK;
+    *c->h_err = 0;
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::string what;
+    if (e & DEV_ERR_GATE_WAIT) what += " a gate wave's wait for a BK slot";
+    if (e & DEV_ERR_LOADER_WAIT) what += std::string(what.empty() ? "" : " and") + " a loader wave's wait for a free BK slot";
+    return fail(c, TFHE_ERR_DEVICE,
+                "blind rotation: slot-counter protocol failure:" + what + " timed out (device error word 0x" +
+                    [&] { char b[16]; std::snprintf(b, sizeof b, "%x", e); return std::string(b); }() +
+                    "); the outputs of the work since the last synchronisation are invalid");
+}
+
+// 64-bit fingerprints of this context's device BK and KSK (k_checksum), synchronous.
+int key_fingerprint(tfhe_gpu_ctx *c, uint64_t &bk, uint64_t &ksk) {
+    auto *d = reinterpret_cast<unsigned long long *>(c->d_err + 2);
+    auto *h = reinterpret_cast<volatile unsigned long long *>(c->h_err + 2);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, launch_checksum(c->d_bk, c->bk_bytes, d, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_err + 2, d, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    bk = *h;
+    HIPCHK(c, launch_checksum(c->d_ksk, c->ksk_bytes, d, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_err + 2, d, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    ksk = *h;
+    return TFHE_OK;
+}
+
 int d2h_sync(tfhe_gpu_ctx *c, void *dst, const void *src, size_t bytes) {
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return TFHE_OK;
+    return sync_check(c);
 }
 
 // TLWELv0.encryptF64 (tlwe.zig:34-49) with DefaultPrng(seed).
@@ -302,7 +348,7 @@ extern "C" {
 
 int tfhe_gpu_abi_version(void) { return TFHE_GPU_ABI_VERSION; }
 
-int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
+int tfhe_gpu_create_on_device(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
     if (!out) return TFHE_ERR_INVALID;
     *out = nullptr;
     std::string why;
@@ -316,7 +362,7 @@ int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
     c->P = *params;
     c->device = device;
     c->K = KParams{(int)params->n, (int)params->N, (int)params->L, (int)params->bgbit, (int)params->basebit,
-                   (int)params->iks_t, 0, ks_stride_for((int)params->n)};
+                   (int)params->iks_t, 0, ks_stride_for((int)params->n), nullptr, 0u};
     int rc = TFHE_OK;
     do {
         hipError_t e = hipSetDevice(device);
@@ -324,6 +370,12 @@ int tfhe_gpu_create(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
         e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
         if (e != hipSuccess) { rc = hip_fail(c, e, "hipStreamCreate"); break; }
         c->stream = c->own_stream;
+        e = hipMalloc((void **)&c->d_err, 64);
+        if (e == hipSuccess) e = hipMemset(c->d_err, 0, 64);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&c->h_err, 64, hipHostMallocDefault);
+        if (e != hipSuccess) { rc = hip_fail(c, e, "device error word"); break; }
+        std::memset(c->h_err, 0, 64);
+        c->K.err = c->d_err;
         rc = build_tables(c, TFHE_TWIDDLES_GLIBC);
     } while (0);
     if (rc != TFHE_OK) {
@@ -340,11 +392,12 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     destroy_shards(c);
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void *p : {(void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
+    for (void *p : {(void *)c->d_err, (void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
                     c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p,
                     c->s_wires.p, c->s_cidx.p, c->s_cops.p})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+    if (c->h_err) (void)hipHostFree(c->h_err);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -353,8 +406,8 @@ const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *c) { return c ? c->err.c_str
 
 int tfhe_gpu_sync(tfhe_gpu_ctx *c) {
     if (!c) return TFHE_ERR_INVALID;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    return sync_check(c);
 }
 
 int tfhe_gpu_set_stream(tfhe_gpu_ctx *c, void *s) {
@@ -380,6 +433,7 @@ int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv
     HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));  // reference leaves k=0 rows undefined
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
+    c->key_from_keygen = false;
     return broadcast_key(c);
 }
 
@@ -414,6 +468,7 @@ int tfhe_gpu_import_key_device(tfhe_gpu_ctx *c, const void *bsk_dev, const void 
     HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
+    c->key_from_keygen = false;
     return broadcast_key(c);
 }
 
@@ -646,6 +701,7 @@ int tfhe_gpu_keygen(tfhe_gpu_ctx *c, uint64_t secret_seed, uint64_t cloud_seed, 
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (ksk_out) std::memcpy(ksk_out, ksk.data(), ksk.size() * sizeof(uint32_t));
     c->has_key = true;
+    c->key_from_keygen = true;
     return broadcast_key(c);
 }
 
@@ -1031,7 +1087,8 @@ static int circuit_eval_one(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *in
         rc = d2h_sync(c, outputs, c->s_out.p, n_outputs * w1 * 4);
         if (rc) return rc;
     } else {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        rc = sync_check(c);
+        if (rc) return rc;
     }
     if (levels_out) *levels_out = max_level;
     return TFHE_OK;
@@ -1060,7 +1117,11 @@ int tfhe_gpu_profile_begin(tfhe_gpu_ctx *c) {
 int tfhe_gpu_profile_end(tfhe_gpu_ctx *c, double *br_ms, double *ks_ms, int *launches) {
     if (!c) return TFHE_ERR_INVALID;
     c->profiling = false;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int rc = sync_check(c);
+    if (rc) {
+        c->ev_used = 0;
+        return rc;
+    }
     double br = 0.0, ks = 0.0;
     for (size_t i = 0; i + 3 <= c->ev_used; i += 3) {
         float a = 0.f, b = 0.f;
@@ -1216,57 +1277,75 @@ int tfhe_lut_generate(const tfhe_params *p, uint32_t m, const uint32_t *f_table,
 // ---- Options ------------------------------------------------------------------
 extern "C" {
 
-int tfhe_gpu_set_option(tfhe_gpu_ctx *c, int key, int64_t v) {
-    if (!c) return TFHE_ERR_INVALID;
-    for (size_t d = 1; d < c->shards.size(); d++) {
-        int rc = tfhe_gpu_set_option(c->shards[d], key, v);
-        if (rc) return fail(c, rc, c->shards[d]->err);
+}  // extern "C"
+
+namespace {
+
+// Range check of one option value, before anything is applied to any device.
+bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
+    bool ok = false;
+    switch (key) {
+    case TFHE_OPT_BR_FORM: ok = v >= 0 && v <= 4; break;
+    case TFHE_OPT_BR_LOADER:
+    case TFHE_OPT_KS_FORM:
+    case TFHE_OPT_KS_NARROW:
+    case TFHE_OPT_CIRCUIT_PACK:
+    case TFHE_OPT_BR_SYNC: ok = v == 0 || v == 1; break;
+    case TFHE_OPT_KS_ITEM_GROUPS: ok = v == 0 || v == 1 || v == 2 || v == 4 || v == 8; break;
+    case TFHE_OPT_KS_SEL_ITEMS: ok = v == 8 || v == 16 || v == 32; break;
+    case TFHE_OPT_ARITH: ok = v == TFHE_ARITH_AUTO || v == TFHE_ARITH_REFERENCE; break;
+    case TFHE_OPT_BR_SPIN_CAP: ok = v >= 0 && v <= 0xFFFFFFFFll; break;
+    case TFHE_OPT_TWIDDLES:
+        ok = v == TFHE_TWIDDLES_GLIBC || v == TFHE_TWIDDLES_FDLIBM;
+        // tfhe_gpu_keygen transformed the resident BK with the current tables:
+        // other tables would no longer match it (a loaded reference key is data
+        // and may be paired with either table)
+        if (ok && c->key_from_keygen && v != c->twiddle_source) {
+            why = "TFHE_OPT_TWIDDLES: the resident key was generated (tfhe_gpu_keygen) with the current FFT tables; "
+                  "set the twiddle source before keygen";
+            return false;
+        }
+        break;
+    default: why = "unknown option key " + std::to_string(key); return false;
     }
+    if (!ok) why = "bad value " + std::to_string(v) + " for option " + std::to_string(key);
+    return ok;
+}
+
+// Apply a checked option to one device's context.
+int apply_option(tfhe_gpu_ctx *c, int key, int64_t v) {
     LaunchOpts &o = c->opts;
     switch (key) {
-    case TFHE_OPT_BR_FORM:
-        if (v < 0 || v > 4) break;
-        o.br_form = (int)v;
-        return TFHE_OK;
-    case TFHE_OPT_BR_LOADER:
-        if (v != 0 && v != 1) break;
-        o.br_loader = (int)v;
-        return TFHE_OK;
-    case TFHE_OPT_KS_FORM:
-        if (v != 0 && v != 1) break;
-        o.ks_form = (int)v;
-        return TFHE_OK;
-    case TFHE_OPT_KS_NARROW:
-        if (v != 0 && v != 1) break;
-        o.ks_narrow = (int)v;
-        return TFHE_OK;
-    case TFHE_OPT_KS_ITEM_GROUPS:
-        if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8) break;
-        o.ks_groups = (int)v;
-        return TFHE_OK;
-    case TFHE_OPT_KS_SEL_ITEMS:
-        if (v != 8 && v != 16 && v != 32) break;
-        o.ks_sel_items = (int)v;
-        return TFHE_OK;
-    case TFHE_OPT_CIRCUIT_PACK:
-        if (v != 0 && v != 1) break;
-        c->circuit_pack = v;
-        return TFHE_OK;
-    case TFHE_OPT_TWIDDLES:
-        if (v != TFHE_TWIDDLES_GLIBC && v != TFHE_TWIDDLES_FDLIBM) break;
-        return build_tables(c, (int)v);
-    case TFHE_OPT_BR_SYNC:
-        if (v != 0 && v != 1) break;
-        o.br_flags = (int)v;
-        return TFHE_OK;
-    case TFHE_OPT_ARITH:
-        if (v != TFHE_ARITH_AUTO && v != TFHE_ARITH_REFERENCE) break;
-        o.arith_strict = v == TFHE_ARITH_REFERENCE;
-        return TFHE_OK;
-    default:
-        return fail(c, TFHE_ERR_INVALID, "unknown option key " + std::to_string(key));
+    case TFHE_OPT_BR_FORM: o.br_form = (int)v; break;
+    case TFHE_OPT_BR_LOADER: o.br_loader = (int)v; break;
+    case TFHE_OPT_KS_FORM: o.ks_form = (int)v; break;
+    case TFHE_OPT_KS_NARROW: o.ks_narrow = (int)v; break;
+    case TFHE_OPT_KS_ITEM_GROUPS: o.ks_groups = (int)v; break;
+    case TFHE_OPT_KS_SEL_ITEMS: o.ks_sel_items = (int)v; break;
+    case TFHE_OPT_CIRCUIT_PACK: c->circuit_pack = v; break;
+    case TFHE_OPT_TWIDDLES: return v == c->twiddle_source ? TFHE_OK : build_tables(c, (int)v);
+    case TFHE_OPT_BR_SYNC: o.br_flags = (int)v; break;
+    case TFHE_OPT_ARITH: o.arith_strict = v == TFHE_ARITH_REFERENCE; break;
+    case TFHE_OPT_BR_SPIN_CAP: c->K.spin_cap = (uint32_t)v; break;
+    default: return TFHE_ERR_INVALID;
     }
-    return fail(c, TFHE_ERR_INVALID, "bad value " + std::to_string(v) + " for option " + std::to_string(key));
+    return TFHE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Validated once, then applied to every device (shards 1.., then the root).
+int tfhe_gpu_set_option(tfhe_gpu_ctx *c, int key, int64_t v) {
+    if (!c) return TFHE_ERR_INVALID;
+    std::string why;
+    if (!option_ok(c, key, v, why)) return fail(c, TFHE_ERR_INVALID, why);
+    for (size_t d = 1; d < c->shards.size(); d++) {
+        const int rc = apply_option(c->shards[d], key, v);
+        if (rc) return fail(c, rc, c->shards[d]->err);
+    }
+    return apply_option(c, key, v);
 }
 
 int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
@@ -1283,6 +1362,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_TWIDDLES: *v = c->twiddle_source; break;
     case TFHE_OPT_ARITH: *v = o.arith_strict ? TFHE_ARITH_REFERENCE : TFHE_ARITH_AUTO; break;
     case TFHE_OPT_BR_SYNC: *v = o.br_flags; break;
+    case TFHE_OPT_BR_SPIN_CAP: *v = c->K.spin_cap; break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;
@@ -1414,10 +1494,24 @@ int broadcast_key(tfhe_gpu_ctx *c) {
         tfhe_gpu_ctx *s = c->shards[d];
         HIPCHK(c, hipSetDevice(s->device));
         HIPCHK(c, hipStreamSynchronize(s->stream));
-        s->has_key = true;
     }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    // every copy must fingerprint like the root's before a shard may use it
+    uint64_t bk0 = 0, ksk0 = 0;
+    int rc = key_fingerprint(c, bk0, ksk0);
+    if (rc) return rc;
+    for (size_t d = 1; d < D; d++) {
+        tfhe_gpu_ctx *s = c->shards[d];
+        uint64_t bk = 0, ksk = 0;
+        rc = key_fingerprint(s, bk, ksk);
+        if (rc) return fail(c, rc, s->err);
+        if (bk != bk0 || ksk != ksk0)
+            return fail(c, TFHE_ERR_HIP, "key broadcast: the copy on device " + std::to_string(s->device) +
+                                             " differs from device " + std::to_string(c->device) + "'s");
+        s->has_key = true;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
     return TFHE_OK;
 }
 
@@ -1449,10 +1543,46 @@ struct Dsu {
     void unite(uint32_t a, uint32_t b) { p[find(a)] = find(b); }
 };
 
-// circuit_eval over the devices: the DAG's connected components (wires joined
-// by gates) go whole to one device each, largest first onto the least-loaded
-// device (bootstrapped gates), so each device evaluates an independent
-// sub-circuit with its own level schedule and no wire crosses devices.
+// Device of every gate (dev_of_gate[g] < D) for circuit_eval_multi: the
+// connected components of the gate DAG under gate-to-gate wires (primary
+// inputs do not join gates: they are replicated), largest first (by
+// bootstrapped gates) onto the least-loaded device.
+void partition_gates(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b,
+                     size_t D, std::vector<uint32_t> &dev_of_gate) {
+    Dsu dsu(std::max<size_t>(n_gates, 1));
+    auto join = [&](size_t g, uint32_t w) {
+        if (w >= n_inputs) dsu.unite((uint32_t)g, (uint32_t)(w - n_inputs));
+    };
+    for (size_t g = 0; g < n_gates; g++) {
+        join(g, in_a[g]);
+        if (ops[g] <= TFHE_GATE_ORYN) join(g, in_b[g]);
+    }
+    std::vector<uint64_t> weight(n_gates, 0);
+    for (size_t g = 0; g < n_gates; g++)
+        if (ops[g] != TFHE_GATE_NOT) weight[dsu.find((uint32_t)g)]++;
+    std::vector<uint32_t> roots;
+    for (size_t g = 0; g < n_gates; g++)
+        if (dsu.find((uint32_t)g) == g) roots.push_back((uint32_t)g);
+    std::stable_sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) { return weight[a] > weight[b]; });
+    std::vector<uint32_t> dev_of_root(n_gates, 0);
+    std::vector<uint64_t> load(D, 0);
+    for (uint32_t r : roots) {
+        const size_t d = std::min_element(load.begin(), load.end()) - load.begin();
+        dev_of_root[r] = (uint32_t)d;
+        load[d] += weight[r];
+    }
+    dev_of_gate.resize(n_gates);
+    for (size_t g = 0; g < n_gates; g++) dev_of_gate[g] = dev_of_root[dsu.find((uint32_t)g)];
+}
+
+// circuit_eval over the devices.  Primary inputs are read-only, so every
+// device gets its own copy of the ones it reads; only gate-to-gate wires tie
+// gates together.  The connected components of the gate DAG under those wires
+// go whole to one device each, largest first onto the least-loaded device
+// (bootstrapped gates), so each device evaluates an independent sub-circuit
+// with its own level schedule and no wire crosses devices.  Config 4's
+// independent AND/OR/XOR gates and MUXes over shared inputs (gates.zig:124-129)
+// spread evenly; one adder (examples/add_two_numbers.zig:24-73) stays whole.
 int circuit_eval_multi(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates, const uint8_t *ops,
                        const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs, const uint32_t *out_wires,
                        uint32_t *outputs, uint32_t *levels_out) {
@@ -1466,63 +1596,51 @@ int circuit_eval_multi(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs,
         for (size_t o = 0; o < n_outputs; o++)
             if (out_wires[o] >= W) return fail(c, TFHE_ERR_INVALID, "output wire out of range");
     }
-    Dsu dsu(W);
-    for (size_t g = 0; g < n_gates; g++) {
-        dsu.unite((uint32_t)(n_inputs + g), in_a[g]);
-        if (ops[g] <= TFHE_GATE_ORYN) dsu.unite((uint32_t)(n_inputs + g), in_b[g]);
-    }
-    std::vector<uint64_t> weight(W, 0);
-    for (size_t g = 0; g < n_gates; g++)
-        if (ops[g] != TFHE_GATE_NOT) weight[dsu.find((uint32_t)(n_inputs + g))]++;
-    std::vector<uint32_t> roots;
-    for (size_t w = 0; w < W; w++)
-        if (dsu.find((uint32_t)w) == w) roots.push_back((uint32_t)w);
-    std::stable_sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) { return weight[a] > weight[b]; });
-    std::vector<uint32_t> dev_of(W, 0);  // per component root
-    std::vector<uint64_t> load(D, 0);
-    for (uint32_t r : roots) {
-        const size_t d = std::min_element(load.begin(), load.end()) - load.begin();
-        dev_of[r] = (uint32_t)d;
-        load[d] += weight[r];
-    }
-    // per-device sub-circuits; wires renumbered: used inputs first, then gates
+    std::vector<uint32_t> dev_of_gate;
+    partition_gates(n_inputs, n_gates, ops, in_a, in_b, D, dev_of_gate);
+    // per-device sub-circuits; wires renumbered: the device's inputs first, then its gates
     struct Sub {
         std::vector<uint32_t> inputs, in_a, in_b, out_wires, out_index;
         std::vector<uint8_t> ops;
         std::vector<uint32_t> outputs;
         uint32_t levels = 0;
+        std::vector<uint32_t> input_id;  // global input -> local id (or none)
     };
     std::vector<Sub> sub(D);
-    std::vector<uint32_t> local(W, 0xFFFFFFFFu);
-    auto dev = [&](uint32_t w) { return dev_of[dsu.find(w)]; };
-    auto use_input = [&](uint32_t w) {
-        if (w < n_inputs && local[w] == 0xFFFFFFFFu) {
-            Sub &s = sub[dev(w)];
-            local[w] = (uint32_t)s.inputs.size();
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    auto gate_dev = [&](size_t g) { return dev_of_gate[g]; };
+    // an output that is a primary input is copied out by device 0
+    auto wire_dev = [&](uint32_t w) { return w < n_inputs ? 0u : gate_dev(w - n_inputs); };
+    auto use_input = [&](uint32_t d, uint32_t w) {
+        if (w >= n_inputs) return;
+        Sub &s = sub[d];
+        if (s.input_id.empty()) s.input_id.assign(n_inputs, NONE);
+        if (s.input_id[w] == NONE) {
+            s.input_id[w] = (uint32_t)s.inputs.size();
             s.inputs.push_back(w);
         }
     };
     for (size_t g = 0; g < n_gates; g++) {
-        use_input(in_a[g]);
-        if (ops[g] <= TFHE_GATE_ORYN) use_input(in_b[g]);
+        use_input(gate_dev(g), in_a[g]);
+        if (ops[g] <= TFHE_GATE_ORYN) use_input(gate_dev(g), in_b[g]);
     }
-    for (size_t o = 0; o < n_outputs; o++) use_input(out_wires[o]);
-    std::vector<uint32_t> gate_count(D, 0);
+    for (size_t o = 0; o < n_outputs; o++) use_input(wire_dev(out_wires[o]), out_wires[o]);
+    std::vector<uint32_t> local_gate(n_gates), gate_count(D, 0);
+    for (size_t g = 0; g < n_gates; g++) local_gate[g] = gate_count[gate_dev(g)]++;
+    auto id = [&](uint32_t d, uint32_t w) {
+        return w < n_inputs ? sub[d].input_id[w] : (uint32_t)sub[d].inputs.size() + local_gate[w - n_inputs];
+    };
     for (size_t g = 0; g < n_gates; g++) {
-        const uint32_t w = (uint32_t)(n_inputs + g), d = dev(w);
-        local[w] = gate_count[d]++;  // final id = #inputs of the device + this
-    }
-    auto id = [&](uint32_t w) { return w < n_inputs ? local[w] : (uint32_t)sub[dev(w)].inputs.size() + local[w]; };
-    for (size_t g = 0; g < n_gates; g++) {
-        Sub &s = sub[dev((uint32_t)(n_inputs + g))];
+        const uint32_t d = gate_dev(g);
+        Sub &s = sub[d];
         s.ops.push_back(ops[g]);
-        s.in_a.push_back(id(in_a[g]));
-        s.in_b.push_back(ops[g] <= TFHE_GATE_ORYN ? id(in_b[g]) : 0u);
+        s.in_a.push_back(id(d, in_a[g]));
+        s.in_b.push_back(ops[g] <= TFHE_GATE_ORYN ? id(d, in_b[g]) : 0u);
     }
     for (size_t o = 0; o < n_outputs; o++) {
-        Sub &s = sub[dev(out_wires[o])];
-        s.out_wires.push_back(id(out_wires[o]));
-        s.out_index.push_back((uint32_t)o);
+        const uint32_t d = wire_dev(out_wires[o]);
+        sub[d].out_wires.push_back(id(d, out_wires[o]));
+        sub[d].out_index.push_back((uint32_t)o);
     }
     std::vector<int> rc(D, TFHE_OK);
     auto run = [&](size_t d) {
@@ -1561,12 +1679,12 @@ int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int 
     std::vector<int> devs(num_devices);
     for (int d = 0; d < num_devices; d++) devs[d] = devices ? devices[d] : d;
     tfhe_gpu_ctx *root = nullptr;
-    int rc = tfhe_gpu_create(params, devs[0], &root);
+    int rc = tfhe_gpu_create_on_device(params, devs[0], &root);
     if (rc) return rc;
     root->shards.push_back(root);
     for (int d = 1; d < num_devices; d++) {
         tfhe_gpu_ctx *s = nullptr;
-        rc = tfhe_gpu_create(params, devs[d], &s);
+        rc = tfhe_gpu_create_on_device(params, devs[d], &s);
         if (rc) {
             tfhe_gpu_destroy(root);
             return rc;
@@ -1580,7 +1698,27 @@ int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int 
     return TFHE_OK;
 }
 
+// SURVEY §8b's entry point: devices 0..num_devices-1 of this node (one device:
+// a plain context on device 0; more: the multi-device context above).
+int tfhe_gpu_create(const tfhe_params *params, int num_devices, tfhe_gpu_ctx **out) {
+    if (!out) return TFHE_ERR_INVALID;
+    *out = nullptr;
+    std::string why;
+    if (num_devices < 1 || !params_ok(params, why)) return TFHE_ERR_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || num_devices > ndev) return TFHE_ERR_HIP;
+    if (num_devices == 1) return tfhe_gpu_create_on_device(params, 0, out);
+    return tfhe_gpu_create_multi(params, num_devices, nullptr, out);
+}
+
 int tfhe_gpu_num_devices(const tfhe_gpu_ctx *c) { return !c ? 0 : c->shards.empty() ? 1 : (int)c->shards.size(); }
+
+int tfhe_gpu_device_bootstraps(const tfhe_gpu_ctx *c, uint64_t *counts, int max_devices) {
+    if (!c || !counts || max_devices < 1) return TFHE_ERR_INVALID;
+    const int D = tfhe_gpu_num_devices(c);
+    for (int d = 0; d < D && d < max_devices; d++) counts[d] = c->shards.empty() ? c->bootstraps : c->shards[d]->bootstraps;
+    return D;
+}
 
 int tfhe_gpu_bootstrap_batch(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
     if (!is_multi(c)) return bootstrap_batch_one(c, in, out, B);
@@ -1667,6 +1805,20 @@ int tfhe_gpu_reencrypt_batch(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const
         while (c->shards[d] != s) d++;
         return reencrypt_batch_one(s, d ? k->peers[d - 1] : k, in + b0 * w, out + b0 * w, n);
     });
+}
+
+int tfhe_circuit_partition(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
+                           const uint32_t *in_b, int num_devices, uint32_t *device_of_gate) {
+    if ((n_gates && (!ops || !in_a || !in_b || !device_of_gate)) || num_devices < 1) return TFHE_ERR_INVALID;
+    if (n_inputs + n_gates > 0xFFFFFFFFull) return TFHE_ERR_INVALID;
+    std::vector<uint32_t> level;
+    std::vector<std::vector<uint32_t>> bs, nots;
+    uint32_t ml = 0;
+    if (schedule_levels(n_inputs, n_gates, ops, in_a, in_b, false, 256, level, ml, bs, nots)) return TFHE_ERR_INVALID;
+    std::vector<uint32_t> dev;
+    partition_gates(n_inputs, n_gates, ops, in_a, in_b, (size_t)num_devices, dev);
+    std::copy(dev.begin(), dev.end(), device_of_gate);
+    return TFHE_OK;
 }
 
 int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates, const uint8_t *ops,

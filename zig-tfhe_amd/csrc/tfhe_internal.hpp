@@ -23,7 +23,20 @@ struct KParams {
     int iks_t;      // key-switch levels
     uint32_t offset;  // decomposition offset (key.zig:121-131)
     int ks_stride;    // words per device KSK row: n+1 rounded up to 4 (16-B aligned rows)
+    // Device error word of the context (sticky, OR of DEV_ERR_* bits; the host
+    // reads it at every synchronisation point and fails the call, never
+    // returning TFHE_OK over the words of a broken launch).
+    uint32_t *err;
+    uint32_t spin_cap;  // polls before a slot-counter wait gives up (TFHE_OPT_BR_SPIN_CAP; 0 = default)
 };
+
+// Bits of the device error word.
+enum DevErr : uint32_t {
+    DEV_ERR_GATE_WAIT = 1u,    // a gate wave's wait for a published BK slot timed out
+    DEV_ERR_LOADER_WAIT = 2u,  // a loader wave's wait for a retired BK slot timed out
+};
+// Default bound of one slot-counter wait (sleep units).
+constexpr uint32_t BR_SPIN_CAP_DEFAULT = 1u << 22;
 
 // Device KSK: the reference's rows [(2^basebit*t*i) + 2^basebit*j + k] of
 // n+1 words (key.zig:148-172), each padded to ks_stride words, plus a tail of
@@ -104,6 +117,8 @@ hipError_t launch_external_product(const KParams &P, const DevTables &T, const d
 // reference BK layout [n][2L][2][N] -> device layout [n][2L][8][64] x {a_re,a_im,b_re,b_im}
 hipError_t launch_bk_permute(const KParams &P, const double *bk_ref, double *bkd, size_t rows,
                              hipStream_t s);
+// 64-bit fingerprint of bytes (a multiple of 16) at p into *out (device), async
+hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s);
 hipError_t launch_bk_unpermute(const KParams &P, const double *bkd, double *bk_ref, size_t rows,
                                hipStream_t s);
 

@@ -21,6 +21,8 @@
 // accumulator update is lane-local.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "tfhe_internal.hpp"
 
 #pragma clang fp contract(off)
@@ -701,9 +703,12 @@ constexpr int BR_LDS_TOTAL =
 // gate wave reads the pair once pub[s] reached 4 x (its use of the slot + 1),
 // and adds 1 to done[s] after its MAC; a loader refills slot s once done[s]
 // shows every gate wave through the previous use.  Gate waves then wait only
-// for data, not for each other.  Every wait is bounded (BR_SPIN_CAP polls):
-// a broken protocol ends the kernel with wrong words, never a hang.
-constexpr uint32_t BR_SPIN_CAP = 1u << 22;
+// for data, not for each other.  Every wait is bounded (KParams::spin_cap
+// polls, BR_SPIN_CAP_DEFAULT = 2^22): a broken protocol never hangs the GPU.
+// A wait that gives up sets the wave's `fail` flag (an SGPR, inside the asm);
+// the wave ORs it into the context's device error word once, at its end
+// (report_wait_failure), and the host fails the call (TFHE_ERR_DEVICE)
+// instead of returning the launch's words.
 // The loader waves poll `done` at s_sleep 12 (~770 cycles) and normal issue
 // priority: their polls (an LDS read and a v_readfirstlane each) had taken
 // issue and LDS slots from the gate wave on the same SIMD.  A refill is due two
@@ -716,8 +721,9 @@ constexpr uint32_t BR_SPIN_CAP = 1u << 22;
 #ifndef TFHE_LOADER_PRIO
 #define TFHE_LOADER_PRIO 0
 #endif
+// `cap` >= 1 polls; on a timeout the loop falls through to `s_mov fail, 1`.
 template <int SLEEP = 1>
-DEV void spin_until_ge(const uint32_t *p, uint32_t target) {
+DEV void spin_until_ge(const uint32_t *p, uint32_t target, uint32_t cap, uint32_t &fail) {
     // the poll loop in asm: every lane reads the same word, the loop stays
     // scalar, and hipcc sees one instruction (a compiler-visible loop here made
     // it hoist address arithmetic out of the step loop and spill)
@@ -734,11 +740,17 @@ DEV void spin_until_ge(const uint32_t *p, uint32_t target) {
         "s_sleep %[sl]\n\t"
         "s_sub_u32 %[cnt], %[cnt], 1\n\t"
         "s_cmp_eq_u32 %[cnt], 0\n\t"
-        "s_cbranch_scc0 1b\n"
+        "s_cbranch_scc0 1b\n\t"
+        "s_mov_b32 %[fail], 1\n"
         "2:"
-        : [v] "=&v"(v), [sv] "=&s"(sv), [cnt] "=&s"(cnt)
-        : [addr] "v"(addr), [tgt] "s"(target), [cap] "s"(BR_SPIN_CAP / SLEEP), [sl] "i"(SLEEP)
+        : [v] "=&v"(v), [sv] "=&s"(sv), [cnt] "=&s"(cnt), [fail] "+s"(fail)
+        : [addr] "v"(addr), [tgt] "s"(target), [cap] "s"(cap), [sl] "i"(SLEEP)
         : "memory", "scc");
+}
+// One lane of a wave whose wait gave up ORs `bit` into the device error word
+// (a vector global atomic).  Called once per wave, after its loop.
+DEV void report_wait_failure(const KParams &P, uint32_t fail, uint32_t bit) {
+    if (fail && P.err && (threadIdx.x & 63) == 0) __hip_atomic_fetch_or(P.err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // One add per wave (lane 0's), without a branch: a divergent `if (lane == 0)`
 // around an atomic split the live ranges of the MAC and spilled 396 B per lane.
@@ -848,8 +860,8 @@ DEV void issue_bk_pair_async(const double2 *__restrict__ src, double2 *slot, int
 template <int L, bool LOADER, bool FU = false, bool FLAGS = false>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
-                  PhaseProf &pp, uint32_t *sync = nullptr, uint32_t k0 = 0, const uint32_t *tA = nullptr,
-                  const uint32_t *tB = nullptr, const C2 *tw0 = nullptr) {
+                  PhaseProf &pp, uint32_t &fail, uint32_t spin_cap, uint32_t *sync = nullptr, uint32_t k0 = 0,
+                  const uint32_t *tA = nullptr, const uint32_t *tB = nullptr, const C2 *tw0 = nullptr) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
         fa[q] = c2(0.0, 0.0);
@@ -884,7 +896,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
         const int slot = (slot0 + rp) & 1;
         if (FLAGS) {  // pair k = k0 + rp is use (k >> 1) of slot k & 1: wait until all 4 loaders published it
             const uint32_t k = k0 + (uint32_t)rp;
-            spin_until_ge(sync + (k & 1), 4u * ((k >> 1) + 1u));
+            spin_until_ge(sync + (k & 1), 4u * ((k >> 1) + 1u), spin_cap, fail);
             __builtin_amdgcn_sched_barrier(0);  // as the barrier did: nothing moves across the wait
         } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the pair's DMA landed
@@ -935,6 +947,9 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
             __builtin_amdgcn_s_setprio(TFHE_LOADER_PRIO);
             const size_t stride = (size_t)L * 2048;
             const uint32_t pairs = (uint32_t)P.n * L;
+            const uint32_t spin = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
+            const uint32_t loader_cap = spin / TFHE_LOADER_SLEEP > 0 ? spin / TFHE_LOADER_SLEEP : 1u;
+            uint32_t fail = 0;
             issue_bk_pair_async(bkd, s_bk, ltid);  // pair 0 into slot 0
             __syncthreads();                       // the gate waves' prologue barrier (counters zeroed)
             PhaseProf lp;  // loader phases (TFHE_PHASE_PROF): 0 DMA landing, 1 waiting for the gates, 2 issue
@@ -945,7 +960,8 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
                 counter_add(s_sync + (k & 1));
                 if (k + 1 < pairs) {
                     const uint32_t k1 = k + 1;
-                    spin_until_ge<TFHE_LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1));  // every gate done with pair k1 - 2
+                    // every gate done with pair k1 - 2
+                    spin_until_ge<TFHE_LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
                     lp.mark(2);
                     issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048,
                                         s_bk + (k1 & 1) * 2048, ltid);
@@ -953,6 +969,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
                 }
             }
             lp.mark(3);
+            report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
 #ifdef TFHE_PHASE_PROF
             if (ltid % 64 == 0)
                 for (int q = 0; q < 4; q++) atomicAdd(&g_phase_cycles[8 + q], (unsigned long long)lp.acc[q]);
@@ -1034,6 +1051,8 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     PhaseProf pp;
     pp.start();
     int at_next = s_at[0];  // a~ of the coming step, read one step ahead
+    uint32_t fail = 0;  // FLAGS: a slot wait gave up (report_wait_failure)
+    const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
 
     for (int i = 0; i < n; i++) {
         pp.mark(0);
@@ -1085,7 +1104,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         C2 fa[8], fb[8];
         at_next = s_at[i + 1 < n ? i + 1 : i];
         br_pairs<L, LOADER, FU, FLAGS>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
-                                       bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp, s_sync,
+                                       bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp, fail, spin_cap, s_sync,
                                        (uint32_t)(L * i), tA, tB, tw0);
         pp.mark(5);
         inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB);
@@ -1102,6 +1121,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     if (t == 0)
         for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], (unsigned long long)pp.acc[k]);
 #endif
+    if (FLAGS) report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
 
     if (!valid) return;
     if (out_mode == BR_OUT_LV1) {
@@ -2606,6 +2626,33 @@ hipError_t launch_external_product(const KParams &P, const DevTables &T, const d
     case 3: hipLaunchKernelGGL(k_external_product<3>, dim3((unsigned)B), dim3(64), 0, s, P, T, bk2, in, out); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// Order-independent 64-bit fingerprint of a device buffer (16-B words; the
+// key buffers are multiples of 16 B): sum over words i of a SplitMix64-style
+// mix of (word, i), one vector atomic add per wave.  Compares the key copies
+// of a multi-device context after its broadcast (HBM-bound, ~35 us per key).
+__global__ __launch_bounds__(256) void k_checksum(const uint4 *__restrict__ p, size_t words16, unsigned long long *out) {
+    unsigned long long acc = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < words16; i += (size_t)gridDim.x * 256) {
+        const uint4 v = p[i];
+        unsigned long long x = (((unsigned long long)v.y << 32) | v.x) ^ (i * 0x9E3779B97F4A7C15ull);
+        unsigned long long y = (((unsigned long long)v.w << 32) | v.z) + (i * 0xD1B54A32D192ED03ull);
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        y = (y ^ (y >> 27)) * 0x94D049BB133111EBull;
+        acc += (x ^ (x >> 31)) + (y ^ (y >> 29));
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(*out), s);
+    if (e != hipSuccess || bytes < 16) return e;
+    const size_t w = bytes / 16;
+    const unsigned blocks = (unsigned)std::min<size_t>((w + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_checksum, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const uint4 *>(p), w, out);
     return hipGetLastError();
 }
 

@@ -23,9 +23,11 @@ LIB_PATH = os.environ.get("TFHE_GPU_LIB") or os.path.join(HERE, "lib", "libtfhe_
 
 # tfhe_gpu_set_option keys / values (include/tfhe_gpu.h TFHE_OPT_*, TFHE_TWIDDLES_*)
 OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_groups": 5, "ks_sel_items": 6,
-           "circuit_pack": 7, "twiddles": 8, "arith": 9, "br_sync": 10}
+           "circuit_pack": 7, "twiddles": 8, "arith": 9, "br_sync": 10, "br_spin_cap": 11}
 OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 0, "ks_narrow": 0, "ks_item_groups": 0,
-                   "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1}
+                   "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1, "br_spin_cap": 0}
+# status codes (include/tfhe_gpu.h TFHE_ERR_*)
+ERR_INVALID, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_IO, ERR_DEVICE = -1, -2, -3, -4, -5, -6
 BR_FORMS = {"auto": 0, "whole": 1, "split": 2, "wide": 3, "pair": 4}
 TWIDDLES_GLIBC, TWIDDLES_FDLIBM = 0, 1
 ARITH_AUTO, ARITH_REFERENCE = 0, 1
@@ -77,13 +79,16 @@ u32p, f64p, u8p, vp = C.POINTER(C.c_uint32), C.POINTER(C.c_double), C.POINTER(C.
 
 _SIGS = {
     "tfhe_gpu_abi_version": (C.c_int, []),
+    "tfhe_gpu_build_id": (C.c_char_p, []),
     "tfhe_gpu_create": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(vp)]),
+    "tfhe_gpu_create_on_device": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(vp)]),
     "tfhe_gpu_destroy": (None, [vp]),
     "tfhe_gpu_last_error": (C.c_char_p, [vp]),
     "tfhe_gpu_sync": (C.c_int, [vp]),
     "tfhe_gpu_set_stream": (C.c_int, [vp, vp]),
     "tfhe_gpu_create_multi": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
     "tfhe_gpu_num_devices": (C.c_int, [vp]),
+    "tfhe_gpu_device_bootstraps": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_int]),
     "tfhe_gpu_set_option": (C.c_int, [vp, C.c_int, C.c_int64]),
     "tfhe_gpu_get_option": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int64)]),
     "tfhe_gpu_last_kernels": (C.c_char_p, [vp]),
@@ -107,6 +112,7 @@ _SIGS = {
                                         C.POINTER(C.c_uint32)]),
     "tfhe_circuit_schedule": (C.c_int, [C.c_size_t, C.c_size_t, u8p, u32p, u32p, C.c_uint32, C.c_int, u32p,
                                         C.POINTER(C.c_uint32)]),
+    "tfhe_circuit_partition": (C.c_int, [C.c_size_t, C.c_size_t, u8p, u32p, u32p, C.c_int, u32p]),
     "tfhe_gpu_blind_rotate_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_bootstrap_lut_batch": (C.c_int, [vp, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_gate_batch_dev": (C.c_int, [vp, vp, vp, vp, vp, C.c_size_t]),
@@ -174,8 +180,17 @@ def _f64(a):
     return a, a.ctypes.data_as(f64p)
 
 
+def build_id() -> str:
+    """tfhe_gpu_build_id: hash of the gfx950 kernels object the loaded library carries."""
+    return load_library().tfhe_gpu_build_id().decode()
+
+
 class TfheError(RuntimeError):
-    pass
+    """A nonzero C-ABI status; `status` is the TFHE_ERR_* code."""
+
+    def __init__(self, msg: str, status: int = 0):
+        super().__init__(msg)
+        self.status = status
 
 
 def fft_tables(N: int = 1024, source: int = TWIDDLES_GLIBC):
@@ -199,15 +214,15 @@ class Context:
         self.params = make_params(params) if not isinstance(params, TfheParams) else params
         h = vp()
         if devices is None:
-            rc = self.lib.tfhe_gpu_create(C.byref(self.params), device, C.byref(h))
-            what = "tfhe_gpu_create"
+            rc = self.lib.tfhe_gpu_create_on_device(C.byref(self.params), device, C.byref(h))
+            what = "tfhe_gpu_create_on_device"
         else:
             devs = (C.c_int * len(devices))(*devices)
             rc = self.lib.tfhe_gpu_create_multi(C.byref(self.params), len(devices), devs, C.byref(h))
             what = "tfhe_gpu_create_multi"
             device = devices[0]
         if rc != 0:
-            raise TfheError(f"{what} failed ({rc})")
+            raise TfheError(f"{what} failed ({rc})", rc)
         self.h = h
         self.device = device
 
@@ -218,6 +233,15 @@ class Context:
     @property
     def num_devices(self) -> int:
         return self.lib.tfhe_gpu_num_devices(self.h)
+
+    def device_bootstraps(self) -> np.ndarray:
+        """Blind rotations launched per device since creation (tfhe_gpu_device_bootstraps)."""
+        n = self.num_devices
+        out = np.zeros(n, np.uint64)
+        rc = self.lib.tfhe_gpu_device_bootstraps(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n)
+        if rc < 0:
+            self.check(rc, "device_bootstraps")
+        return out
 
     def set_option(self, name: str, value: int):
         """tfhe_gpu_set_option (kernel forms, twiddle source; OPTIONS)."""
@@ -237,13 +261,18 @@ class Context:
 
     @contextlib.contextmanager
     def options(self, **kw):
-        """Temporarily set options (A/B runs, tests); defaults restored on exit."""
+        """Temporarily set options (A/B runs, tests).  On exit each option named
+        in `kw` goes back to the value it had on entry (not to its default:
+        a `twiddles` choice made before the block survives it)."""
+        before = {k: self.get_option(k) for k in kw}
         try:
             for k, v in kw.items():
                 self.set_option(k, v)
             yield self
         finally:
-            self.reset_options()
+            for k, v in before.items():
+                if self.get_option(k) != v:
+                    self.set_option(k, v)
 
     def last_kernels(self) -> str:
         """Kernel names of this context's last bootstrap launch (tfhe_gpu_last_kernels)."""
@@ -262,7 +291,7 @@ class Context:
 
     def check(self, rc: int, what: str):
         if rc != 0:
-            raise TfheError(f"{what}: status {rc}: {self.lib.tfhe_gpu_last_error(self.h).decode()}")
+            raise TfheError(f"{what}: status {rc}: {self.lib.tfhe_gpu_last_error(self.h).decode()}", rc)
 
     @property
     def n1(self) -> int:
@@ -828,6 +857,20 @@ class Circuit:
         if rc:
             raise TfheError(f"circuit_schedule: status {rc}")
         return levels[:ops.size], depth.value
+
+    def partition(self, num_devices: int):
+        """The device of every gate a multi-device context's circuit_eval uses
+        (host only, tfhe_circuit_partition)."""
+        lib = load_library()
+        ops = np.array(self.ops, np.uint8)
+        ia, iap = _u32(np.array(self.ia, np.uint32))
+        ib, ibp = _u32(np.array(self.ib, np.uint32))
+        dev = np.zeros(max(len(self.ops), 1), np.uint32)
+        rc = lib.tfhe_circuit_partition(self.n_inputs, ops.size, ops.ctypes.data_as(u8p), iap, ibp, num_devices,
+                                        dev.ctypes.data_as(u32p))
+        if rc:
+            raise TfheError(f"circuit_partition: status {rc}")
+        return dev[:ops.size]
 
     def run(self, ctx: "Context", inputs):
         inputs = np.asarray(inputs, np.uint32).reshape(-1, ctx.params.n + 1)
