@@ -118,6 +118,10 @@ int tfhe_gpu_num_devices(const tfhe_gpu_ctx *ctx);
  * created (counts[d] for device d < max_devices, in create order); returns the
  * number of devices.  Shows where a sharded batch or circuit ran. */
 int tfhe_gpu_device_bootstraps(const tfhe_gpu_ctx *ctx, uint64_t *counts, int max_devices);
+/* Items whose blind rotation the fused arithmetic's margin guard sent to the
+ * reference-tree recompute since the context was created (a value rounded
+ * within 1/8 of a tie), as of the last synchronisation. */
+int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
 
 /* ---- Options (kernel forms and table sources; default = the measured-
  * fastest forms).  Set on a context before use; a multi-device context
@@ -142,11 +146,13 @@ enum {
                                      error word (0 = default, 2^22 sleep units; fault-injection tests
                                      set a few polls to see TFHE_ERR_DEVICE come back) */
 };
-/* TFHE_ARITH_AUTO (default): where the exact external product is an integer
- * polynomial the f64 evaluation rounds to (the L=3 / Bg=2^6 sets: the
- * reference's own rounding error stays below ~0.1) the kernels
- * use fused multiply-adds, which round to the same integers with fewer
- * instructions; elsewhere (UINT4) the reference's expression trees.
+/* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
+ * runs fused multiply-adds in the reference's operation order, with a margin
+ * guard: every value it rounds must lie within 3/8 of an integer (the fused
+ * and the reference's values differ by <= 2^-6); an item that
+ * rounded anything closer to a tie is recomputed in the reference's expression
+ * trees in the same stream (tfhe_gpu_near_tie_items counts them), so both
+ * round to the same integers.  UINT4: the reference's trees.
  * TFHE_ARITH_REFERENCE: the reference's expression trees everywhere. */
 enum { TFHE_ARITH_AUTO = 0, TFHE_ARITH_REFERENCE = 1 };
 /* The two libm candidates a Zig build of the reference can bind @cos/@sin to

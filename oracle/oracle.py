@@ -89,6 +89,8 @@ class Oracle:
         L.oracle_set_trig_source.argtypes = [C.c_int]
         L.oracle_get_trig_source.restype = C.c_int
         L.oracle_take_round_error.restype = C.c_double
+        L.oracle_capture_rounded.restype = C.c_size_t
+        L.oracle_capture_rounded.argtypes = [C.c_void_p, C.c_size_t]
         L.oracle_set_fused.argtypes = [C.c_int]
         L.oracle_get_fused.restype = C.c_int
 
@@ -99,9 +101,24 @@ class Oracle:
     def trig_source(self) -> int:
         return self.lib.oracle_get_trig_source()
 
-    def set_fused(self, fused: bool):
-        """Arithmetic of the transforms / MAC: reference expression trees or fused multiply-adds."""
-        self.lib.oracle_set_fused(int(bool(fused)))
+    def set_fused(self, fused):
+        """Arithmetic of the transforms / MAC: reference expression trees (False / 0),
+        fused multiply-adds (True / 1), or "guarded" (2): fused with the kernels'
+        margin guard, a blind rotation that rounds near a tie redone in the
+        reference's trees (the MI355X default at the 128/80-bit sets)."""
+        self.lib.oracle_set_fused(2 if fused == 2 else int(bool(fused)))
+
+    def rounded_values(self, fn, cap=1 << 16):
+        """Run fn() and return the pre-rounding values its inverse transforms
+        rounded, in output order (coefficient i, then i + N/2 of each transform)."""
+        buf = np.zeros(cap, np.float64)
+        self.lib.oracle_capture_rounded(buf.ctypes.data, cap)
+        try:
+            fn()
+        finally:
+            n = self.lib.oracle_capture_rounded(None, 0)
+        v = buf[:n].reshape(-1, 512, 2)  # [transform][i][re, im] -> coefficient order i ++ i + 512
+        return np.concatenate([v[:, :, 0], v[:, :, 1]], axis=1).ravel()
 
     def take_round_error(self) -> float:
         """max |x - round(x)| of the inverse transforms run on this thread since the last call."""

@@ -239,9 +239,19 @@ double oracle_trig_sin(double x, int source) { return source == 1 ? fd_sin(x) : 
  * L=3 / Bg=2^6 sets (there the exact external product is an
  * integer polynomial and both forms round to it).  Twiddle values and the
  * operation order are unchanged.  Test infrastructure, like the rest. */
-static int g_fused = 0;
-void oracle_set_fused(int fused) { g_fused = fused ? 1 : 0; }
-int oracle_get_fused(void) { return g_fused; }
+/* 2 = "guarded": fused, plus the kernels' margin guard (torus_from_f64_guarded,
+ * tfhe_kernels.hip): a blind rotation that rounds a value with
+ * rint(4v + 2) = 0 mod 4 (|v - rint(v)| >= 3/8, via the same f64 add as the
+ * kernel) is redone in the reference's trees — the MI355X default.  FUSED is
+ * the arithmetic in force on this thread (a guarded recompute forces 0). */
+static int g_fused = 0, g_guard = 0;
+static __thread int tl_force_ref = 0, tl_near = 0;
+#define FUSED (g_fused && !tl_force_ref)
+void oracle_set_fused(int fused) {
+    g_fused = fused ? 1 : 0;
+    g_guard = fused == 2;
+}
+int oracle_get_fused(void) { return g_fused ? (g_guard ? 2 : 1) : 0; }
 
 /* ======================================================================== */
 /* FFT — fft.zig KlemsaProcessor                                             */
@@ -306,7 +316,7 @@ static void radix2_fft(cplx *data, size_t n, int inverse) {
             for (size_t j = 0; j < len / 2; j++) {
                 cplx u = data[i + j];
                 cplx x = data[i + j + len / 2];
-                if (g_fused) {                             /* a = u + x*w, b = 2u - a */
+                if (FUSED) {                               /* a = u + x*w, b = 2u - a */
                     double a_re = fma(x.re, w_re, fma(-x.im, w_im, u.re));
                     double a_im = fma(x.re, w_im, fma(x.im, w_re, u.im));
                     data[i + j].re = a_re;
@@ -360,7 +370,7 @@ void oracle_ifft(uint32_t N, const uint32_t *in, double *out) {
         double in_re = (double)(int32_t)in[i];
         double in_im = (double)(int32_t)in[i + n2];
         double w_re = tre[i], w_im = tim[i];
-        if (g_fused) {
+        if (FUSED) {
             buf[i].re = fma(in_re, w_re, -(in_im * w_im));
             buf[i].im = fma(in_re, w_im, in_im * w_re);
         } else {
@@ -389,6 +399,20 @@ double oracle_take_round_error(void) {
     return e;
 }
 
+/* Optional capture of the values the inverse transform rounds (test evidence
+ * for DESIGN.md §6.1: the distance between the reference's and the fused
+ * arithmetic's pre-rounding values).  oracle_capture_rounded(buf, cap) starts
+ * appending to buf (NULL stops); returns the count captured so far. */
+static __thread double *tl_cap = NULL;
+static __thread size_t tl_cap_n = 0, tl_cap_max = 0;
+size_t oracle_capture_rounded(double *buf, size_t cap) {
+    size_t n = tl_cap_n;
+    tl_cap = buf;
+    tl_cap_max = cap;
+    tl_cap_n = 0;
+    return n;
+}
+
 void oracle_fft(uint32_t N, const double *in, uint32_t *out) {
     size_t n2 = N / 2;
     cplx *buf = (cplx *)malloc(sizeof(cplx) * n2);
@@ -403,17 +427,29 @@ void oracle_fft(uint32_t N, const double *in, uint32_t *out) {
     for (size_t i = 0; i < n2; i++) {
         double w_re = tre[i], w_im = tim[i];
         double f_re = buf[i].re, f_im = buf[i].im;
-        double tmp_re = (g_fused ? fma(f_re, w_re, f_im * w_im) : f_re * w_re + f_im * w_im) * normalization;
-        double tmp_im = (g_fused ? fma(f_im, w_re, -(f_re * w_im)) : f_im * w_re - f_re * w_im) * normalization;
+        double tmp_re = (FUSED ? fma(f_re, w_re, f_im * w_im) : f_re * w_re + f_im * w_im) * normalization;
+        double tmp_im = (FUSED ? fma(f_im, w_re, -(f_re * w_im)) : f_im * w_re - f_re * w_im) * normalization;
         /* reference: @round, half away from zero.  Fused mode restates the fused
          * kernels' conversion (to_torus<SMALL, true>, tfhe_kernels.hip): round to
          * nearest even (there, v + 1.5*2^52).  Inside the exact-integer regime the
          * two agree: v is within ~0.1 of an integer, so no tie occurs. */
-        int64_t rr = (int64_t)(g_fused ? nearbyint(tmp_re) : round(tmp_re));
-        int64_t ri = (int64_t)(g_fused ? nearbyint(tmp_im) : round(tmp_im));
+        int64_t rr = (int64_t)(FUSED ? nearbyint(tmp_re) : round(tmp_re));
+        int64_t ri = (int64_t)(FUSED ? nearbyint(tmp_im) : round(tmp_im));
+        if (FUSED && g_guard) {
+            double s_re = tmp_re + 1688849860263936.5, s_im = tmp_im + 1688849860263936.5;  /* 1.5*2^50 + 0.5 */
+            uint64_t b_re, b_im;
+            memcpy(&b_re, &s_re, 8);
+            memcpy(&b_im, &s_im, 8);
+            if ((b_re & 3u) == 0 || (b_im & 3u) == 0) tl_near = 1;
+        }
         double e_re = fabs(tmp_re - round(tmp_re)), e_im = fabs(tmp_im - round(tmp_im));
         if (e_re > tl_round_err) tl_round_err = e_re;
         if (e_im > tl_round_err) tl_round_err = e_im;
+        if (tl_cap && tl_cap_n + 2 <= tl_cap_max) {  /* output order: i, then i + n2 */
+            tl_cap[tl_cap_n + 0] = tmp_re;
+            tl_cap[tl_cap_n + 1] = tmp_im;
+            tl_cap_n += 2;
+        }
         out[i] = (uint32_t)(int32_t)rr;
         out[i + n2] = (uint32_t)(int32_t)ri;
     }
@@ -490,7 +526,7 @@ void oracle_poly_mul_with_xk(uint32_t N, const uint32_t *a, uint32_t k, uint32_t
 static void fma_in_fd(size_t n2, double *res, const double *a, const double *b) {
     for (size_t i = 0; i < n2; i++) {
         double a_re = a[i], a_im = a[i + n2], b_re = b[i], b_im = b[i + n2];
-        if (g_fused) {  /* res += a*b*0.5 by fma; b*0.5 is exact */
+        if (FUSED) {  /* res += a*b*0.5 by fma; b*0.5 is exact */
             res[i] = fma(a_re, b_re * 0.5, fma(-a_im, b_im * 0.5, res[i]));
             res[i + n2] = fma(a_re, b_im * 0.5, fma(a_im, b_re * 0.5, res[i + n2]));
             continue;
@@ -547,16 +583,23 @@ void oracle_blind_rotate(const oracle_params *p, const uint32_t *src, const uint
     uint32_t b_tilda = 2 * N - (uint32_t)(((uint64_t)src[p->n] + round_half) >> shift);
     uint32_t *res2 = (uint32_t *)malloc(sizeof(uint32_t) * 2 * N);
     uint32_t *nxt = (uint32_t *)malloc(sizeof(uint32_t) * 2 * N);
-    oracle_poly_mul_with_xk(N, testvec, b_tilda, acc);
-    oracle_poly_mul_with_xk(N, testvec + N, b_tilda, acc + N);
     size_t row = (size_t)2 * p->L * 2 * N;
-    for (uint32_t i = 0; i < p->n; i++) {
-        uint32_t a_tilda = (uint32_t)(((uint64_t)src[i] + round_half) >> shift);
-        oracle_poly_mul_with_xk(N, acc, a_tilda, res2);
-        oracle_poly_mul_with_xk(N, acc + N, a_tilda, res2 + N);
-        oracle_cmux(p, acc, res2, bk + i * row, offset, nxt);
-        memcpy(acc, nxt, sizeof(uint32_t) * 2 * N);
+    tl_near = 0;
+    for (int pass = 0; pass < 2; pass++) {  /* guarded mode: a second pass in the reference's trees */
+        oracle_poly_mul_with_xk(N, testvec, b_tilda, acc);
+        oracle_poly_mul_with_xk(N, testvec + N, b_tilda, acc + N);
+        for (uint32_t i = 0; i < p->n; i++) {
+            uint32_t a_tilda = (uint32_t)(((uint64_t)src[i] + round_half) >> shift);
+            oracle_poly_mul_with_xk(N, acc, a_tilda, res2);
+            oracle_poly_mul_with_xk(N, acc + N, a_tilda, res2 + N);
+            oracle_cmux(p, acc, res2, bk + i * row, offset, nxt);
+            memcpy(acc, nxt, sizeof(uint32_t) * 2 * N);
+        }
+        if (!(FUSED && g_guard && tl_near)) break;
+        tl_force_ref = 1;
     }
+    tl_force_ref = 0;
+    tl_near = 0;
     free(res2); free(nxt);
 }
 

@@ -148,6 +148,10 @@ void oracle_set_fused(int fused);
 int oracle_get_fused(void);
 /* max |x - round(x)| rounded by oracle_fft on this thread since the last call (then reset) */
 double oracle_take_round_error(void);
+/* Start capturing the inverse transforms' pre-rounding values into buf (pairs
+ * (re_i, im_i) per coefficient i < N/2; NULL stops); returns the count captured
+ * by the previous capture. */
+size_t oracle_capture_rounded(double *buf, size_t cap);
 
 #ifdef __cplusplus
 }

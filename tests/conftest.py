@@ -63,3 +63,19 @@ def keys_uint4(oracle):
 
 def rng(seed=0):
     return np.random.default_rng(seed)
+
+
+def crafted_near_tie_case(oracle, p, seed=3):
+    """(testvec, reference-layout BK, TLWELv0) of a blind rotation whose fused
+    arithmetic rounds near a tie and parts from the reference:
+    constant test vector offset/2 (so tmp = -offset and every digit is -32 at
+    step 0 with a~_0 = N, b~ = 2N), BK[0]'s rows all FFT(2^31 - 1), the other
+    steps zero (their external products are exactly 0)."""
+    off = oracle.decomposition_offset(p)
+    tv = np.full(2 * p.N, off // 2, np.uint32)
+    bk = np.zeros((p.n, 2 * p.L, 2, p.N))
+    spec = oracle.ifft(np.full(p.N, (1 << 31) - 1, np.uint32))
+    bk[0, :, :, :] = spec
+    ct = rng(seed).integers(0, 1 << 32, p.n + 1, dtype=np.uint64).astype(np.uint32)
+    ct[0], ct[p.n] = 1 << 31, 0  # a~_0 = N, b~ = 2N (identity)
+    return tv, bk, ct

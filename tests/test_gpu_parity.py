@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import tfhe_amd
-from conftest import get_keys, rng
+from conftest import crafted_near_tie_case, get_keys, rng
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -512,3 +512,39 @@ def test_slot_counters_and_barrier_agree_at_full_size(oracle):
             assert "slot counters" not in c.last_kernels()
         assert np.array_equal(flags, bar)
         assert np.array_equal(sk.decrypt_bool(flags), ~(a_bits.astype(bool) & b_bits.astype(bool)))
+
+
+@pytest.mark.parametrize("form", ["auto", "whole", "split", "pair", "wide"])
+def test_margin_guard_recomputes_near_ties(oracle, form):
+    """the crafted blind rotation whose unguarded fused arithmetic
+    parts from the reference (conftest.crafted_near_tie_case; the oracle's fused
+    mode differs from its reference mode there) comes back with the REFERENCE's
+    words from every fused form: the item rounded a value within 1/8 of a tie, the
+    margin guard flagged it and the reference-tree recompute redid it
+    (tfhe_gpu_near_tie_items counts it).  Five honest items in the same batch
+    are untouched (not counted) and bit-exact too."""
+    p = get_keys(oracle, "128").p
+    tv, bk, ct = crafted_near_tie_case(oracle, p)
+    ksk = np.zeros((p.N * p.iks_t * (1 << p.basebit), p.n + 1), np.uint32)
+    off = oracle.decomposition_offset(p)
+    c = tfhe_amd.Context("128", 0)
+    try:
+        c.load_cloud_key(off, tv, bk, ksk)
+        g = rng(4242)
+        cts = np.concatenate([u32rand(g, 2, p.n + 1), ct[None], u32rand(g, 3, p.n + 1)])
+        want, fused = [], []
+        try:
+            for mode, dst in ((0, want), (1, fused)):
+                oracle.set_fused(mode)
+                dst.extend(oracle.blind_rotate(p, x, tv, bk, off) for x in cts)
+        finally:
+            oracle.set_fused(0)
+        want, fused = np.array(want), np.array(fused)
+        assert not np.array_equal(fused[2], want[2]) and np.array_equal(fused[[0, 1, 3, 4, 5]], want[[0, 1, 3, 4, 5]])
+        before = c.near_tie_items()
+        with c.options(br_form=form):
+            got = c.blind_rotate_batch(cts, tv)
+        assert c.near_tie_items() - before == 1
+        assert np.array_equal(got, want)
+    finally:
+        c.close()

@@ -11,7 +11,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import get_keys, rng
+from conftest import crafted_near_tie_case, get_keys, rng
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -220,6 +220,167 @@ def test_fused_arithmetic_differs_where_inexact(oracle, keys_uint4):
     finally:
         oracle.set_fused(0)
     assert not np.array_equal(a, b)
+
+
+def _tmp_with_fields(oracle, p, fields):
+    """TRLWE words whose decomposition (offset included) has digit field
+    fields[k] (0..63, digit = field - 32) at every level of coefficient k."""
+    f = np.asarray(fields, np.uint64)
+    v = (f << 26) | (f << 20) | (f << 14)
+    return ((v - oracle.decomposition_offset(p)) % (1 << 32)).astype(np.uint32)
+
+
+def _ext_values(oracle, p, rows, x, mode):
+    """Pre-rounding values and words of externalProductWithFft with integer rows
+    (2L, 2, N) in `mode` (0 reference trees, 1 fused)."""
+    off = oracle.decomposition_offset(p)
+    trgsw = np.array([[oracle.ifft((r[0] % (1 << 32)).astype(np.uint32)),
+                       oracle.ifft((r[1] % (1 << 32)).astype(np.uint32))] for r in rows])
+    try:
+        oracle.set_fused(mode)
+        out = {}
+        v = oracle.rounded_values(lambda: out.setdefault("w", oracle.external_product(p, trgsw, x, off)))
+    finally:
+        oracle.set_fused(0)
+    return v, out["w"]
+
+
+def _exact(oracle, p, rows, x):
+    dig = oracle.decomposition(p, x, oracle.decomposition_offset(p)).view(np.int32).astype(np.int64)
+    def neg(d, r):
+        c = np.convolve(d, r.astype(np.int64))
+        c = np.concatenate([c, [0]])
+        return c[:1024] - c[1024:]
+    a = sum(neg(dig[i], rows[i][0]) for i in range(2 * p.L))
+    b = sum(neg(dig[i], rows[i][1]) for i in range(2 * p.L))
+    return np.concatenate([a, b])
+
+
+def test_worst_case_magnitudes_reference_and_fused_trees(oracle):
+    """DESIGN.md §6.1, the exact-integer regime at its limits (128-bit: L = 3,
+    Bg = 2^6, |digit| <= 32, |row| <= 2^31, |ExtProd| <= 6*1024*32*2^31 = 2^48.6).
+    (1) Worst magnitude, structured rows: every row the constant 2^31 - 1 and every
+    digit -32 (or 31).  Neither the reference's trees nor the fused ones round to
+    the exact integer (no a-priori bound below 1/2 holds for EITHER), and the two
+    part: their pre-rounding values differ by up to 0.31 there.
+    (2) Random full-range rows (the distribution keygen gives every BK row) with
+    extreme digit patterns: both trees exact, errors below 1/4, and the trees'
+    pre-rounding values within 2^-6 of each other."""
+    from oracle import params
+    p = params("128")
+    g = rng(606)
+    R = (1 << 31) - 1
+    rows_kinds = {
+        "const": lambda: np.full(1024, R, np.int64),
+        "alternating": lambda: np.where(np.arange(1024) % 2 == 0, R, -R),
+        "random_sign": lambda: np.where(g.random(1024) < 0.5, R, -R),
+        "random_full": lambda: g.integers(-(1 << 31), 1 << 31, 1024),
+    }
+    fields_kinds = {"all_-32": lambda: np.zeros(1024), "all_31": lambda: np.full(1024, 63),
+                    "random_extreme": lambda: np.where(g.random(1024) < 0.5, 0, 63),
+                    "alternating": lambda: np.where(np.arange(1024) % 2 == 0, 0, 63)}
+    delta = {}
+    for rk, rf in rows_kinds.items():
+        for fk, ff in fields_kinds.items():
+            rows = np.array([[rf(), rf()] for _ in range(2 * p.L)])
+            x = np.concatenate([_tmp_with_fields(oracle, p, ff()), _tmp_with_fields(oracle, p, ff())])
+            exact = _exact(oracle, p, rows, x)
+            v0, w0 = _ext_values(oracle, p, rows, x, 0)
+            v1, w1 = _ext_values(oracle, p, rows, x, 1)
+            assert np.abs(exact).max() <= 6 * 1024 * 32 * R
+            delta[rk, fk] = float(np.abs(v0 - v1).max())
+            want = (exact % (1 << 32)).astype(np.uint32)
+            if rk == "const" and fk in ("all_-32", "all_31"):  # (1): |ExtProd| ~ 2^48.4
+                assert np.abs(exact).max() > 2 ** 48.3
+                assert np.abs(v0 - exact).max() >= 0.5 and np.abs(v1 - exact).max() >= 0.5
+                assert not np.array_equal(w0, want) and not np.array_equal(w1, want)
+                assert not np.array_equal(w0, w1)
+            if rk == "random_full":  # (2)
+                assert np.array_equal(w0, want) and np.array_equal(w1, want)
+                assert np.abs(v0 - exact).max() < 0.25 and np.abs(v1 - exact).max() < 0.25
+                assert delta[rk, fk] <= 2.0 ** -6
+    assert max(delta.values()) > 0.25  # (1): the structured worst case
+
+
+def test_aligned_adversarial_digits_part_the_trees(oracle):
+    """Against random full-range rows (a keygen'd BK), digits chosen by someone who
+    knows the (public) key: the three levels of a's and of b's digits each aligned
+    in sign with one of the six rows at one output k, the largest |ExtProd| such a
+    key admits (2^47.6).  The reference's own rounding error then reaches 1/2 (it
+    misses the exact integer at ~0.1 % of outputs) and the reference's and the
+    fused trees round some coefficients differently.  Their pre-rounding values
+    stay within 1/8 of each other (measured max 0.094 over 3.3 M such outputs,
+    DESIGN.md §6.1), so the kernels' margin guard (|v - rint(v)| >= 3/8 ->
+    recompute in the reference's trees) flags every coefficient where they part."""
+    from oracle import params
+    p = params("128")
+    off = oracle.decomposition_offset(p)
+    g = rng(607)
+
+    def tmp3(f0, f1, f2):
+        v = (f0.astype(np.uint64) << 26) | (f1.astype(np.uint64) << 20) | (f2.astype(np.uint64) << 14)
+        return ((v - off) % (1 << 32)).astype(np.uint32)
+
+    delta, part, mag = 0.0, 0, 0
+    for trial in range(400):
+        rows = g.integers(-(1 << 31), 1 << 31, (2 * p.L, 2, 1024))
+        k = int(g.integers(0, 1024))
+        j = np.arange(1024)
+        m, w = (k - j) % 1024, np.where(j <= k, 1, -1)
+        F = [np.where(w * np.sign(rows[i][trial % 2][m]) > 0, 63, 0) for i in range(2 * p.L)]
+        x = np.concatenate([tmp3(F[0], F[1], F[2]), tmp3(F[3], F[4], F[5])])
+        mag = max(mag, int(np.abs(_exact(oracle, p, rows, x)).max()))
+        v0, w0 = _ext_values(oracle, p, rows, x, 0)
+        v1, w1 = _ext_values(oracle, p, rows, x, 1)
+        delta = max(delta, float(np.abs(v0 - v1).max()))
+        differ = w0 != w1
+        part += int(differ.sum())
+        # the kernel's guard: v + (1.5*2^50 + 1/2) by one f64 add, mantissa bits 1:0 == 0
+        near = ((v1 + 1688849860263936.5).view(np.uint64) & np.uint64(3)) == 0
+        assert not (differ & ~near).any()  # every parting coefficient is flagged
+    assert mag > 2 ** 47.5
+    assert delta < 0.125
+    assert part > 0
+
+
+def test_guarded_fused_rotation_equals_reference_on_a_crafted_near_tie(oracle):
+    """A blind rotation where the unguarded fused arithmetic parts from the
+    reference: constant test vector V = offset/2 (tmp = -offset, every digit -32
+    at step 0 with a~_0 = N, b~ = 2N), BK[0] rows all FFT(2^31 - 1), the other
+    steps zero.  Fused vs reference: words differ.  Guarded (oracle mode 2 = the
+    MI355X default): the rotation rounded near a tie, was redone in the
+    reference's trees, and equals the reference.  tests/test_gpu_parity.py runs
+    the same case on the GPU."""
+    from oracle import params
+    p = params("128")
+    off = oracle.decomposition_offset(p)
+    tv, bk, ct = crafted_near_tie_case(oracle, p)
+    out = {}
+    try:
+        for mode in (0, 1, 2):
+            oracle.set_fused(mode)
+            out[mode] = oracle.blind_rotate(p, ct, tv, bk, off)
+    finally:
+        oracle.set_fused(0)
+    assert (out[1] != out[0]).sum() > 0
+    assert np.array_equal(out[2], out[0])
+
+
+def test_guarded_mode_is_the_fused_mode_on_honest_rotations(oracle, keys128):
+    """Honest blind rotations (the seeded cloud key, random ciphertexts): nothing
+    rounds near a tie, the guard never fires, and all three modes agree."""
+    k = keys128
+    g = rng(608)
+    for _ in range(2):
+        ct = g.integers(0, 1 << 32, k.p.n + 1, dtype=np.uint64).astype(np.uint32)
+        out = {}
+        try:
+            for mode in (0, 1, 2):
+                oracle.set_fused(mode)
+                out[mode] = oracle.blind_rotate(k.p, ct, k.ck.testvec, k.ck.bk, k.ck.offset)
+        finally:
+            oracle.set_fused(0)
+        assert np.array_equal(out[0], out[1]) and np.array_equal(out[0], out[2])
 
 
 def test_twiddle_source_changes_gates_only_where_inexact():

@@ -52,6 +52,7 @@ struct tfhe_gpu_ctx {
     // scratch, grown on demand
     DevBuf s_a, s_b, s_out, s_lv1, s_ops, s_tv, s_tmp;
     DevBuf s_wires, s_cidx, s_cops;  // circuit evaluator: wire table, gather indices, op codes
+    DevBuf s_ties;                   // near-tie flags (KParams::tie_flags), one byte per item, zero between launches
     // device timing (tfhe_gpu_profile_begin/end): 3 events per bootstrap launch
     bool profiling = false;
     std::vector<hipEvent_t> events;
@@ -61,6 +62,7 @@ struct tfhe_gpu_ctx {
     int64_t circuit_pack = 1;
     int64_t twiddle_source = TFHE_TWIDDLES_GLIBC;
     bool key_from_keygen = false;  // the resident BK was transformed with this context's tables
+    uint64_t near_tie_items = 0;   // items the margin guard recomputed (device err[1], read by sync_check)
     const char *last_br = "", *last_ks = "";
     std::string last_kernels;
     // multi-device context (tfhe_gpu_create_multi): shards[0] is this context
@@ -178,6 +180,13 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
     if (B == 0) return TFHE_OK;
     int rc = ensure(c, c->s_lv1, B * 1025 * sizeof(uint32_t));
     if (rc) return rc;
+    if (c->s_ties.bytes < B) {  // the flags are all zero between launches: a new buffer starts zeroed
+        rc = ensure(c, c->s_ties, B);
+        if (rc) return rc;
+        HIPCHK(c, hipMemsetAsync(c->s_ties.p, 0, c->s_ties.bytes, c->stream));
+    }
+    KParams K = c->K;
+    K.tie_flags = (uint8_t *)c->s_ties.p;
     uint32_t *lv1 = key_switch ? (uint32_t *)c->s_lv1.p : out;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     if (c->profiling) {
@@ -190,7 +199,7 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
         c->ev_used += 3;
         HIPCHK(c, hipEventRecord(ev[0], c->stream));
     }
-    HIPCHK(c, launch_blind_rotate(c->K, tables(c), ops, a, b, idx, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
+    HIPCHK(c, launch_blind_rotate(K, tables(c), ops, a, b, idx, testvec_dev ? testvec_dev : c->d_testvec, c->d_bk,
                                   lv1, out_mode, B, c->stream, c->opts, &c->last_br));
     c->bootstraps += B;
     if (ev[1]) HIPCHK(c, hipEventRecord(ev[1], c->stream));
@@ -213,8 +222,9 @@ int h2d(tfhe_gpu_ctx *c, DevBuf &buf, const void *src, size_t bytes) {
 // on the stream, so the one synchronisation covers both; a reported error is
 // cleared, and the context stays usable.
 int sync_check(tfhe_gpu_ctx *c) {
-    HIPCHK(c, hipMemcpyAsync(c->h_err, c->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_err, c->d_err, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->near_tie_items = c->h_err[1];
     const uint32_t e = *c->h_err;
     if (!e) return TFHE_OK;
     *c->h_err = 0;
@@ -362,7 +372,7 @@ int tfhe_gpu_create_on_device(const tfhe_params *params, int device, tfhe_gpu_ct
     c->P = *params;
     c->device = device;
     c->K = KParams{(int)params->n, (int)params->N, (int)params->L, (int)params->bgbit, (int)params->basebit,
-                   (int)params->iks_t, 0, ks_stride_for((int)params->n), nullptr, 0u};
+                   (int)params->iks_t, 0, ks_stride_for((int)params->n), nullptr, 0u, nullptr, 0};
     int rc = TFHE_OK;
     do {
         hipError_t e = hipSetDevice(device);
@@ -393,7 +403,7 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)c->d_err, (void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
-                    c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p,
+                    c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p, c->s_ties.p,
                     c->s_wires.p, c->s_cidx.p, c->s_cops.p})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -1712,6 +1722,14 @@ int tfhe_gpu_create(const tfhe_params *params, int num_devices, tfhe_gpu_ctx **o
 }
 
 int tfhe_gpu_num_devices(const tfhe_gpu_ctx *c) { return !c ? 0 : c->shards.empty() ? 1 : (int)c->shards.size(); }
+
+int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *c, uint64_t *count) {
+    if (!c || !count) return TFHE_ERR_INVALID;
+    uint64_t n = c->near_tie_items;
+    for (size_t d = 1; d < c->shards.size(); d++) n += c->shards[d]->near_tie_items;
+    *count = n;
+    return TFHE_OK;
+}
 
 int tfhe_gpu_device_bootstraps(const tfhe_gpu_ctx *c, uint64_t *counts, int max_devices) {
     if (!c || !counts || max_devices < 1) return TFHE_ERR_INVALID;

@@ -25,9 +25,17 @@ struct KParams {
     int ks_stride;    // words per device KSK row: n+1 rounded up to 4 (16-B aligned rows)
     // Device error word of the context (sticky, OR of DEV_ERR_* bits; the host
     // reads it at every synchronisation point and fails the call, never
-    // returning TFHE_OK over the words of a broken launch).
+    // returning TFHE_OK over the words of a broken launch).  err[1] counts the
+    // items the margin guard's recompute redid (cumulative).
     uint32_t *err;
     uint32_t spin_cap;  // polls before a slot-counter wait gives up (TFHE_OPT_BR_SPIN_CAP; 0 = default)
+    // Near-tie flags of the fused arithmetic's margin guard,
+    // one byte per item of a blind-rotation launch, all zero between launches:
+    // a fused kernel sets tie_flags[g] when item g rounded a value within 1/8 of
+    // a tie; the reference-tree recompute launched after it (fallback = 1) redoes
+    // the flagged items' workgroups and clears their flags.
+    uint8_t *tie_flags;
+    int fallback;
 };
 
 // Bits of the device error word.

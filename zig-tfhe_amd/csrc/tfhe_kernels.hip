@@ -473,21 +473,44 @@ DEV uint32_t torus_from_f64_small(double v) {
     return (uint32_t)__double_as_longlong(s);
 }
 
-// Fused kernels (FU, the exact-integer regime of DESIGN.md §6.1): v lies within
-// ~0.1 of the integer I the reference rounds its own value to, so every
-// rounding of v gives I and no tie can occur.  One add does it: v + 1.5*2^52
-// rounds to nearest and leaves I mod 2^32 in the low mantissa word (|v| < 2^51).
-// 1 f64 op per coefficient instead of 6 (2 trunc + 4 add).
+// Fused kernels (FU, the exact-integer regime of DESIGN.md §6.1), with the
+// margin guard.  The fused value v and the reference's value differ by far
+// less than 1/8 (measured <= 2^-6), so wherever v is more than
+// 1/8 from a tie both round to the same integer.  One add rounds v + 0.5 to a
+// multiple of 1/4: s = v + (1.5*2^50 + 0.5) (|v| < 2^49), whose mantissa is
+// 2^51 + Q with Q = rint(4v + 2).  Q >> 2 (mantissa bits 33..2, one
+// v_alignbit) is rint(v) and Q mod 4 = 0 exactly when |v - rint(v)| >= 3/8:
+// `near` keeps the minimum of (Q mod 4) over the launch, and a 0 sends the
+// item to the reference-tree recompute (near_tie_flag, k_blind_rotate FALLBACK).
+DEV uint32_t torus_from_f64_guarded(double v, uint32_t &near) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v + 1688849860263936.5);
+    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    near = min(near, lo & 3u);
+    return __builtin_amdgcn_alignbit(hi, lo, 2);
+}
+
+// Unguarded fused conversion (TFHE_FU_UNGUARDED A/B builds only): v + 1.5*2^52
+// rounds to nearest and leaves rint(v) mod 2^32 in the low mantissa word.
 DEV uint32_t torus_from_f64_near_integer(double v) {
     return (uint32_t)__double_as_longlong(v + 6755399441055744.0);
 }
 
 template <bool SMALL, bool FU = false>
-DEV uint32_t to_torus(double v) {
-#ifndef TFHE_FU_EXACT_ROUND
+DEV uint32_t to_torus(double v, uint32_t &near) {
+#ifdef TFHE_FU_UNGUARDED
     if (FU) return torus_from_f64_near_integer(v);
+#else
+    if (FU) return torus_from_f64_guarded(v, near);
 #endif
     return SMALL ? torus_from_f64_small(v) : torus_from_f64(v);
+}
+// Initial value of a `near` accumulator: no near tie seen.
+constexpr uint32_t NEAR_NONE = 3u;
+// End of a fused item: if any lane of this wave rounded near a tie, flag item g
+// (one byte, a vector store; the flag is rare, the ballot is one SALU compare).
+DEV void near_tie_flag(const KParams &P, uint32_t near, size_t g, bool valid) {
+    if (__builtin_amdgcn_ballot_w64(near == 0u) != 0 && valid && P.tie_flags && (threadIdx.x & 63) == 0)
+        P.tie_flags[g] = 1;
 }
 
 // decompositionIntoStorage digit (trgsw.zig:207-217); `x` already has the
@@ -609,7 +632,7 @@ DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 
 // CMUX add acc' = ExtProd + acc (trgsw.zig:277-281), lane-local.
 template <bool SMALL, int TS, bool ONEBUF = false, bool FU = false, class TW>
 DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const C2 *tws, int t,
-                         uint32_t *accA, uint32_t *accB) {
+                         uint32_t *accA, uint32_t *accB, uint32_t &near) {
     C2 e[2][8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -625,10 +648,10 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
         const C2 w = tws[q * TS];
         untwist_out<false, FU>(e[0][q], w, ra, ia);
         untwist_out<false, FU>(e[1][q], w, rb, ib);
-        accA[q] += to_torus<SMALL, FU>(ra);
-        accA[q + 8] += to_torus<SMALL, FU>(ia);
-        accB[q] += to_torus<SMALL, FU>(rb);
-        accB[q + 8] += to_torus<SMALL, FU>(ib);
+        accA[q] += to_torus<SMALL, FU>(ra, near);
+        accA[q + 8] += to_torus<SMALL, FU>(ia, near);
+        accB[q] += to_torus<SMALL, FU>(rb, near);
+        accB[q + 8] += to_torus<SMALL, FU>(ib, near);
     }
 }
 
@@ -941,6 +964,13 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     double2 *s_bk = reinterpret_cast<double2 *>(smem);
     // FLAGS: pub[2], done[2] (zeroed by the gate waves before the prologue barrier)
     uint32_t *s_sync = reinterpret_cast<uint32_t *>(smem + BR_LDS_TOTAL - BR_LDS_SYNC);
+    if (!FU && P.fallback) {  // reference-tree recompute: only workgroups with a flagged item
+        const size_t g0 = (size_t)blockIdx.x * BR_WAVES;
+        uint32_t any = 0;
+        for (int k = 0; k < BR_WAVES; k++)
+            if (g0 + k < B) any |= P.tie_flags[g0 + k];
+        if (!any) return;  // uniform over the workgroup: every wave reads the same flags
+    }
     if constexpr (LOADER && FLAGS) {
         if (w >= BR_WAVES) {  // loader wave, counter protocol (see spin_until_ge)
             const int ltid = tid - 64 * BR_WAVES;
@@ -1051,6 +1081,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     PhaseProf pp;
     pp.start();
     int at_next = s_at[0];  // a~ of the coming step, read one step ahead
+    uint32_t near = NEAR_NONE;  // FU: margin guard (torus_from_f64_guarded)
     uint32_t fail = 0;  // FLAGS: a slot wait gave up (report_wait_failure)
     const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
 
@@ -1107,7 +1138,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
                                        bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp, fail, spin_cap, s_sync,
                                        (uint32_t)(L * i), tA, tB, tw0);
         pp.mark(5);
-        inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB);
+        inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB, near);
         wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) {
@@ -1122,6 +1153,14 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], (unsigned long long)pp.acc[k]);
 #endif
     if (FLAGS) report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
+    if (FU) near_tie_flag(P, near, g, valid);
+    // recompute: every wave of the workgroup read the flags before the prologue
+    // barrier, so this item's flag can be cleared now; err[1] counts the items
+    // recomputed (tfhe_gpu_near_tie_items)
+    if (!FU && P.fallback && valid && t == 0 && P.tie_flags[g]) {
+        P.tie_flags[g] = 0;
+        __hip_atomic_fetch_add(P.err + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 
     if (!valid) return;
     if (out_mode == BR_OUT_LV1) {
@@ -1242,6 +1281,7 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
     const C2 *spec_0 = s_xg;        // spectrum of row 2r (wave 0 of the item)
     const C2 *spec_1 = s_xg + 512;  // spectrum of row 2r+1 (wave 1)
     const uint32_t *s_tmp_item = reinterpret_cast<const uint32_t *>(base + (2 * gs) * BS_LDS_ACC);
+    uint32_t near = NEAR_NONE;  // FU: margin guard
     wave_sync();
 
     for (int i = 0; i < n; i++) {
@@ -1306,14 +1346,15 @@ __global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
         for (int q = 0; q < 8; q++) {
             double re, im;
             untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-            acc[q] += to_torus<SMALL, FU>(re);
-            acc[q + 8] += to_torus<SMALL, FU>(im);
+            acc[q] += to_torus<SMALL, FU>(re, near);
+            acc[q + 8] += to_torus<SMALL, FU>(im, near);
         }
         wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) s_acc[t + 64 * m] = acc[m];
         wave_sync();
     }
+    if (FU) near_tie_flag(P, near, g, valid);
 
     if (!valid) return;
     if (out_mode == BR_OUT_LV1) {
@@ -1444,6 +1485,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
     T.init(s_tw, TT);
     const C2 *twist_t = s_twist + t;
     int at_next = s_at[0];
+    uint32_t near = NEAR_NONE;  // FU: margin guard
 
     for (int i = 0; i < n; i++) {
         const int at = __builtin_amdgcn_readfirstlane(at_next);
@@ -1525,11 +1567,12 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
         for (int q = 0; q < 8; q++) {
             double re, im;
             untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-            acc[q] += to_torus<SMALL, FU>(re);
-            acc[q + 8] += to_torus<SMALL, FU>(im);
+            acc[q] += to_torus<SMALL, FU>(re, near);
+            acc[q + 8] += to_torus<SMALL, FU>(im, near);
         }
     }
 
+    if (FU) near_tie_flag(P, near, g, valid);
     // epilogue through this wave's buffer: acc_h at [0, 1024)
 #pragma unroll
     for (int m = 0; m < 16; m++) s_xw[t + 64 * m] = acc[m];
@@ -1624,6 +1667,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     __syncthreads();
 
     int at_next = s_at[0];  // a~ read one step ahead (its wait would drain every LDS op)
+    uint32_t near = NEAR_NONE;  // FU: margin guard (the inverse waves)
     PhaseProf pp;  // development timing (TFHE_PHASE_PROF), per wave
     pp.start();
     for (int i = 0; i < n; i++) {
@@ -1696,8 +1740,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
             for (int q = 0; q < 8; q++) {
                 double re, im;
                 untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-                pa[t + 64 * q] += to_torus<SMALL, FU>(re);
-                pa[t + 64 * q + 512] += to_torus<SMALL, FU>(im);
+                pa[t + 64 * q] += to_torus<SMALL, FU>(re, near);
+                pa[t + 64 * q + 512] += to_torus<SMALL, FU>(im, near);
             }
         }
         pp.mark(5);
@@ -1708,6 +1752,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     if (t == 0)
         for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[w * 8 + k], (unsigned long long)pp.acc[k]);
 #endif
+    if (FU) near_tie_flag(P, near, g, true);
 
     if (w != 0) return;
     if (out_mode == BR_OUT_LV1) {
@@ -2212,7 +2257,8 @@ __global__ __launch_bounds__(64) void k_external_product(KParams P, DevTables TT
     }
     C2 fa[8], fb[8];
     ext_pairs_global<L>(tA, tB, bkrow, P.bgbit, T, twl, s_x, t, fa, fb);
-    inverse_and_add<false, 1>(fa, fb, s_x, T, twl, t, accA, accB);
+    uint32_t near = NEAR_NONE;
+    inverse_and_add<false, 1>(fa, fb, s_x, T, twl, t, accA, accB, near);
     uint32_t *o = out + (size_t)blockIdx.x * 2048;
 #pragma unroll
     for (int m = 0; m < 16; m++) {
@@ -2300,15 +2346,20 @@ static bool launch_pair(const KParams &P, const DevTables &T, const uint8_t *ops
     return false;
 }
 
+// |external product| <= 2L * N * Bg/2 * 2^31 below 2^49: the SMALL conversions
+// and the fused arithmetic's guarded conversion hold (the L=3 / Bg=2^6 sets:
+// 2^48.6; UINT4: 2^63, never)
+static bool small_products(const KParams &P) {
+    return std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 49);
+}
+
 static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
                                hipStream_t s, char form, const LaunchOpts &O, const char **used) {
     if (B == 0) return hipSuccess;
     const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
-    // |external product| <= 2L * N * Bg/2 * 2^31: the 8-op exact conversion
-    // needs it below 2^51 (true for the L=3 / Bg=2^6 sets, false for UINT4)
-    const bool small = std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 50);
+    const bool small = small_products(P);
     // form: 'W' latency (8 waves per item), 's' split (2 waves per item),
     // 'w' whole (1 wave per item; loader waves unless LaunchOpts::br_loader = 0)
     const bool split = form == 's';
@@ -2428,11 +2479,10 @@ double blind_rotate_cost(size_t B, size_t cus) {
     return (double)(B / round) + wide(tail);
 }
 
-hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
-                               const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
-                               const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
-                               hipStream_t s, const LaunchOpts &O, const char **used) {
-    if (B == 0) return hipSuccess;
+static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T, const uint8_t *ops,
+                                            const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                                            const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
+                                            size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (O.br_form) {  // forced form (TFHE_OPT_BR_FORM): the whole batch in one launch
         const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : 'w';
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
@@ -2445,12 +2495,50 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     const size_t main = B - tail;
     hipError_t e = launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, main, s, 'w', O, used);
     if (e != hipSuccess) return e;
-    // the tail: items main..B-1 (their ops / idx entries / inputs / outputs)
+    // the tail: items main..B-1 (their ops / idx entries / inputs / outputs / near-tie flags)
     const size_t in_words = (size_t)P.n + 1;
     const size_t out_words = out_mode == BR_OUT_LV1 ? (size_t)P.N + 1 : out_mode == BR_OUT_TRLWE ? 2 * (size_t)P.N : in_words;
-    return launch_blind_rotate_form(P, T, ops ? ops + main : nullptr, idx ? in_a : in_a + main * in_words,
+    KParams Q = P;
+    if (Q.tie_flags) Q.tie_flags += main;
+    return launch_blind_rotate_form(Q, T, ops ? ops + main : nullptr, idx ? in_a : in_a + main * in_words,
                                     idx ? in_b : (in_b ? in_b + main * in_words : nullptr), idx ? idx + 2 * main : nullptr,
                                     testvec, bkd, out + main * out_words, out_mode, tail, s, 'W', O, nullptr);
+}
+
+// The margin guard's recompute: the whole form in the
+// reference's expression trees over the same B items, whose workgroups return
+// at once unless one of their 4 items was flagged by the fused launch.
+static hipError_t launch_br_recompute(const KParams &P, const DevTables &T, const uint8_t *ops, const uint32_t *in_a,
+                                      const uint32_t *in_b, const uint32_t *idx, const uint32_t *testvec,
+                                      const double2 *bk2, uint32_t *out, int out_mode, size_t B, hipStream_t s) {
+    KParams Q = P;
+    Q.fallback = 1;
+    const dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(64 * BR_WAVES * 2);
+    switch (P.L) {
+    case 1: hipLaunchKernelGGL((k_blind_rotate<1, true, true, false, true>), grid, block, 0, s, Q, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B); break;
+    case 2: hipLaunchKernelGGL((k_blind_rotate<2, true, true, false, true>), grid, block, 0, s, Q, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B); break;
+    case 3: hipLaunchKernelGGL((k_blind_rotate<3, true, true, false, true>), grid, block, 0, s, Q, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
+                               const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                               const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
+                               hipStream_t s, const LaunchOpts &O, const char **used) {
+    if (B == 0) return hipSuccess;
+    KParams Q = P;
+    Q.fallback = 0;
+    const bool fused = small_products(P) && O.arith_strict == 0;
+    if (!fused) Q.tie_flags = nullptr;
+    hipError_t e = launch_blind_rotate_forms(Q, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, O, used);
+#ifdef TFHE_FU_UNGUARDED  // A/B builds: the fused arithmetic without its margin guard
+    return e;
+#endif
+    if (e != hipSuccess || !fused || !Q.tie_flags) return e;
+    return launch_br_recompute(Q, T, ops, in_a, in_b, idx, testvec, reinterpret_cast<const double2 *>(bkd), out,
+                               out_mode, B, s);
 }
 
 // lane-form key switch over an input of n_in coefficients (+ b); false if

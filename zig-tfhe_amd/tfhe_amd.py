@@ -89,6 +89,7 @@ _SIGS = {
     "tfhe_gpu_create_multi": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
     "tfhe_gpu_num_devices": (C.c_int, [vp]),
     "tfhe_gpu_device_bootstraps": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_int]),
+    "tfhe_gpu_near_tie_items": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
     "tfhe_gpu_set_option": (C.c_int, [vp, C.c_int, C.c_int64]),
     "tfhe_gpu_get_option": (C.c_int, [vp, C.c_int, C.POINTER(C.c_int64)]),
     "tfhe_gpu_last_kernels": (C.c_char_p, [vp]),
@@ -233,6 +234,13 @@ class Context:
     @property
     def num_devices(self) -> int:
         return self.lib.tfhe_gpu_num_devices(self.h)
+
+    def near_tie_items(self) -> int:
+        """Items the margin guard recomputed in the reference's expression trees
+        (tfhe_gpu_near_tie_items), as of the last synchronisation."""
+        v = C.c_uint64()
+        self.check(self.lib.tfhe_gpu_near_tie_items(self.h, C.byref(v)), "near_tie_items")
+        return v.value
 
     def device_bootstraps(self) -> np.ndarray:
         """Blind rotations launched per device since creation (tfhe_gpu_device_bootstraps)."""
