@@ -516,13 +516,13 @@ def test_slot_counters_and_barrier_agree_at_full_size(oracle):
 
 @pytest.mark.parametrize("form", ["auto", "whole", "split", "pair", "wide"])
 def test_margin_guard_recomputes_near_ties(oracle, form):
-    """the crafted blind rotation whose unguarded fused arithmetic
-    parts from the reference (conftest.crafted_near_tie_case; the oracle's fused
-    mode differs from its reference mode there) comes back with the REFERENCE's
-    words from every fused form: the item rounded a value within 1/8 of a tie, the
-    margin guard flagged it and the reference-tree recompute redid it
-    (tfhe_gpu_near_tie_items counts it).  Five honest items in the same batch
-    are untouched (not counted) and bit-exact too."""
+    """under a crafted key (conftest.crafted_near_tie_case) the
+    unguarded fused arithmetic parts from the reference (the oracle's fused mode
+    differs from its reference mode).  Every fused form returns the REFERENCE's
+    words: the items that rounded a value within 1/8 of a tie were flagged by
+    the margin guard and redone by the reference-tree recompute, which
+    tfhe_gpu_near_tie_items counts.  (Honest batches never trigger it:
+    test_margin_guard_quiet_on_honest_batches.)"""
     p = get_keys(oracle, "128").p
     tv, bk, ct = crafted_near_tie_case(oracle, p)
     ksk = np.zeros((p.N * p.iks_t * (1 << p.basebit), p.n + 1), np.uint32)
@@ -540,11 +540,27 @@ def test_margin_guard_recomputes_near_ties(oracle, form):
         finally:
             oracle.set_fused(0)
         want, fused = np.array(want), np.array(fused)
-        assert not np.array_equal(fused[2], want[2]) and np.array_equal(fused[[0, 1, 3, 4, 5]], want[[0, 1, 3, 4, 5]])
+        parted = int((fused != want).any(axis=1).sum())
+        assert not np.array_equal(fused[2], want[2]) and parted >= 1
         before = c.near_tie_items()
         with c.options(br_form=form):
             got = c.blind_rotate_batch(cts, tv)
-        assert c.near_tie_items() - before == 1
+        assert parted <= c.near_tie_items() - before <= len(cts)
         assert np.array_equal(got, want)
     finally:
         c.close()
+
+
+def test_margin_guard_quiet_on_honest_batches(oracle):
+    """The seeded key and a 1,024-gate NAND batch of fresh encryptions (the
+    headline shape): no value comes within 3/8 of a tie (honest rotations stay
+    within ~0.11 of an integer), nothing is recomputed."""
+    c, k = ctx_for(oracle, "128")
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    g = rng(5151)
+    a, b = g.integers(0, 2, 1024).astype(np.uint8), g.integers(0, 2, 1024).astype(np.uint8)
+    A, B = sk.encrypt_bool(a, seed0=51_000), sk.encrypt_bool(b, seed0=52_000)
+    before = c.near_tie_items()
+    out = c.gate_batch(np.zeros(1024, np.uint8), A, B)
+    assert c.near_tie_items() == before
+    assert np.array_equal(sk.decrypt_bool(out), ~(a.astype(bool) & b.astype(bool)))

@@ -5,12 +5,22 @@
 // (fft.zig:293-443), then sampleExtractIndex (trlwe.zig:146-162) and
 // identityKeySwitching (trgsw.zig:471-502).
 //
-// Bit-exactness contract: every f64 operation of the
-// reference is performed with the same operands, the same expression tree and
-// round-to-nearest, no FMA contraction (file-wide `fp contract(off)` plus
-// -ffp-contract=off), twiddles uploaded from the host (never sin/cos on the
-// device).  Exact power-of-two rescalings (×2 in ifft1024, ×0.5 in
-// fmaInFd1024 and fft1024) are folded, which leaves every result bit-identical.
+// Bit-exactness contract.  Two arithmetics, selected per
+// instantiation (template parameter FU):
+//  - reference trees (FU = false; UINT4 always, every set under
+//    TFHE_ARITH_REFERENCE, the near-tie recompute): every f64 operation of the
+//    reference with the same operands, the same expression tree and
+//    round-to-nearest; the compiler never contracts (file-wide
+//    `fp contract(off)` plus -ffp-contract=off);
+//  - fused (FU = true; the default at the L=3 / Bg=2^6 sets): explicit fused
+//    multiply-adds (fmad below, __builtin_fma) in the reference's operation
+//    order, with a margin guard on every rounding: an item whose fused values
+//    come within 1/8 of a tie is recomputed in the reference trees
+//    (torus_from_f64_guarded, launch_br_recompute), so both give the
+//    reference's integers.
+// Twiddles are uploaded from the host (never sin/cos on the device).  Exact
+// power-of-two rescalings (×2 in ifft1024, ×0.5 in fmaInFd1024 and fft1024)
+// are folded, which leaves every result bit-identical.
 //
 // FFT mapping: one wavefront owns one 512-point complex transform (N=1024
 // negacyclic), 8 complex values per lane, three radix-2^3 register passes
