@@ -1,0 +1,81 @@
+// Host <-> device copy rates on the GPU box, for the host-buffer pipeline
+// (DESIGN.md §2.1): pageable vs pinned hipMemcpyAsync and host memcpy into
+// pinned staging with 1..8 threads, at the 1,024-gate batch's sizes.
+//   hipcc -O2 -o tools/bin/copy_bw tools/copy_bw.cpp -lpthread && tools/bin/copy_bw
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+#define CK(x)                                                               \
+    do {                                                                    \
+        hipError_t e_ = (x);                                                \
+        if (e_ != hipSuccess) {                                             \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));    \
+            return 1;                                                       \
+        }                                                                   \
+    } while (0)
+
+int main() {
+    const size_t in_bytes = 2 * 1024 * 701 * 4, out_bytes = 1024 * 701 * 4;
+    std::vector<char> src(in_bytes, 1), dst(out_bytes, 0);
+    char *pin_in = nullptr, *pin_out = nullptr, *dev = nullptr;
+    CK(hipHostMalloc((void **)&pin_in, in_bytes, hipHostMallocDefault));
+    CK(hipHostMalloc((void **)&pin_out, out_bytes, hipHostMallocDefault));
+    CK(hipMalloc((void **)&dev, in_bytes));
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    auto rate = [](size_t b, double t) { return b / t / 1e9; };
+    for (int rep = 0; rep < 3; rep++) {
+        double t0 = now();
+        CK(hipMemcpyAsync(dev, src.data(), in_bytes, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));
+        double t1 = now();
+        CK(hipMemcpyAsync(dev, pin_in, in_bytes, hipMemcpyHostToDevice, s));
+        CK(hipStreamSynchronize(s));
+        double t2 = now();
+        CK(hipMemcpyAsync(dst.data(), dev, out_bytes, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        double t3 = now();
+        CK(hipMemcpyAsync(pin_out, dev, out_bytes, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        double t4 = now();
+        std::printf("H2D %.1f MB: pageable %.3f ms (%.1f GB/s), pinned %.3f ms (%.1f GB/s); D2H %.1f MB: pageable %.3f ms "
+                    "(%.1f GB/s), pinned %.3f ms (%.1f GB/s)\n",
+                    in_bytes / 1e6, (t1 - t0) * 1e3, rate(in_bytes, t1 - t0), (t2 - t1) * 1e3, rate(in_bytes, t2 - t1),
+                    out_bytes / 1e6, (t3 - t2) * 1e3, rate(out_bytes, t3 - t2), (t4 - t3) * 1e3, rate(out_bytes, t4 - t3));
+    }
+    for (int th : {1, 2, 4, 8}) {
+        double best = 1e9;
+        for (int rep = 0; rep < 5; rep++) {
+            double t0 = now();
+            std::vector<std::thread> v;
+            for (int k = 0; k < th; k++)
+                v.emplace_back([&, k] {
+                    const size_t a = in_bytes * k / th, b = in_bytes * (k + 1) / th;
+                    std::memcpy(pin_in + a, src.data() + a, b - a);
+                });
+            for (auto &x : v) x.join();
+            best = std::min(best, now() - t0);
+        }
+        std::printf("memcpy pageable -> pinned %.1f MB, %d thread(s): %.3f ms (%.1f GB/s)\n", in_bytes / 1e6, th, best * 1e3,
+                    rate(in_bytes, best));
+    }
+    // pipelined: 4 chunks, memcpy chunk k then its H2D, on one thread
+    {
+        double t0 = now();
+        const size_t c = in_bytes / 4;
+        for (int k = 0; k < 4; k++) {
+            std::memcpy(pin_in + k * c, src.data() + k * c, c);
+            CK(hipMemcpyAsync(dev + k * c, pin_in + k * c, c, hipMemcpyHostToDevice, s));
+        }
+        CK(hipStreamSynchronize(s));
+        std::printf("staged H2D in 4 chunks, 1 thread: %.3f ms\n", (now() - t0) * 1e3);
+    }
+    return 0;
+}
