@@ -142,9 +142,12 @@ enum {
     TFHE_OPT_BR_SYNC = 10,        /* whole form with loader waves: 1 per-slot LDS counters (default: gate
                                      waves wait for their data, not for each other), 0 a workgroup
                                      barrier per BK row pair */
-    TFHE_OPT_BR_SPIN_CAP = 11     /* polls before one slot-counter wait gives up and sets the device
+    TFHE_OPT_BR_SPIN_CAP = 11,    /* polls before one slot-counter wait gives up and sets the device
                                      error word (0 = default, 2^22 sleep units; fault-injection tests
                                      set a few polls to see TFHE_ERR_DEVICE come back) */
+    TFHE_OPT_HOST_PIPELINE = 12   /* host-buffer bootstrap / gate / LUT batches of >= 4 x #CUs items:
+                                     1 (default) chunked through pinned staging on 4 streams (copies
+                                     overlap the kernels), 0 one H2D -> kernels -> D2H sequence */
 };
 /* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
  * runs fused multiply-adds in the reference's operation order, with a margin

@@ -8,8 +8,11 @@
 #include <rccl/rccl.h>  // types and prototypes only: librccl is dlopen'ed on first multi-device key load
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -25,6 +28,62 @@ struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
 };
+
+// Persistent host workers of one context (the host-buffer pipeline's staging
+// copies and its per-stream enqueueing): run(n, f) calls
+// f(0..n-1) on n workers (n <= size) and returns when all are done.
+class WorkerPool {
+  public:
+    explicit WorkerPool(int n) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread &t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    void run(int n, const std::function<void(int)> &f) {
+        std::unique_lock<std::mutex> g(m_);
+        job_ = &f;
+        active_ = n;
+        pending_ = n;
+        gen_++;
+        cv_.notify_all();
+        done_.wait(g, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)> *f = nullptr;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || (gen_ != seen && i < active_); });
+                if (stop_) return;
+                seen = gen_;
+                f = job_;
+            }
+            (*f)(i);
+            std::lock_guard<std::mutex> g(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    int active_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+constexpr int PIPE_STREAMS = 4;  // concurrent chunks of the host-buffer pipeline (HIP's 4 hardware queues)
 
 struct tfhe_gpu_ctx {
     tfhe_params P{};
@@ -72,6 +131,13 @@ struct tfhe_gpu_ctx {
     bool distinct_devices = true;    // RCCL needs each device once; else D2D copies
     // blind rotations launched on this device since creation (tfhe_gpu_device_bootstraps)
     uint64_t bootstraps = 0;
+    // host-buffer pipeline (pipelined_bootstrap): streams, pinned staging, workers
+    hipStream_t pipe[PIPE_STREAMS] = {};
+    hipEvent_t pipe_ev = nullptr;
+    char *pin_in = nullptr, *pin_out = nullptr;
+    size_t pin_in_bytes = 0, pin_out_bytes = 0;
+    std::unique_ptr<WorkerPool> workers;
+    int64_t pipeline = 1;  // TFHE_OPT_HOST_PIPELINE
     std::vector<ncclComm_t> comms;   // one communicator per shard, created on the first key broadcast
 };
 
@@ -408,6 +474,12 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->h_err) (void)hipHostFree(c->h_err);
+    c->workers.reset();
+    for (hipStream_t &p : c->pipe)
+        if (p) (void)hipStreamDestroy(p);
+    if (c->pipe_ev) (void)hipEventDestroy(c->pipe_ev);
+    if (c->pin_in) (void)hipHostFree(c->pin_in);
+    if (c->pin_out) (void)hipHostFree(c->pin_out);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -715,10 +787,126 @@ int tfhe_gpu_keygen(tfhe_gpu_ctx *c, uint64_t secret_seed, uint64_t cloud_seed, 
     return broadcast_key(c);
 }
 
+}  // extern "C"
+
+namespace {
+
+int ensure_pinned(tfhe_gpu_ctx *c, char *&p, size_t &have, size_t bytes) {
+    if (have >= bytes) return TFHE_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    have = 0;
+    HIPCHK(c, hipHostMalloc((void **)&p, bytes, hipHostMallocDefault));
+    have = bytes;
+    return TFHE_OK;
+}
+
+// Host-buffer bootstrap of B >= one whole-form round, pipelined (DESIGN.md
+// §2.1): the batch is cut into chunks of #CUs items (a quarter round: #CUs/4
+// workgroups of the whole form).  Worker s owns stream s and chunks s, s+S, ...;
+// per chunk it copies the caller's inputs into pinned staging, then enqueues
+// H2D -> blind rotation (whole form; the guard's recompute) -> key switch ->
+// D2H on its stream, so chunk k+1's copies run while chunks <= k compute and
+// the S streams' kernels share the CUs.  Each worker then waits for its stream
+// and copies its chunks' outputs to the caller.  ops / b / tv_dev may be NULL.
+int pipelined_bootstrap(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b,
+                        const uint32_t *tv_dev, uint32_t *out, size_t B) {
+    const size_t w = tlwe0_words(c), wb = w * 4, chunk = device_cus();
+    const size_t nch = (B + chunk - 1) / chunk;
+    const int S = (int)std::min<size_t>(PIPE_STREAMS, nch);
+    // staging layout per item: op byte region, then a, then b (all chunks contiguous)
+    const size_t ops_bytes = ops ? (B + 15) / 16 * 16 : 0, a_bytes = B * wb, b_bytes = b ? B * wb : 0;
+    int rc = ensure_pinned(c, c->pin_in, c->pin_in_bytes, ops_bytes + a_bytes + b_bytes);
+    if (!rc) rc = ensure_pinned(c, c->pin_out, c->pin_out_bytes, B * wb);
+    if (!rc && ops) rc = ensure(c, c->s_ops, B);
+    if (!rc) rc = ensure(c, c->s_a, B * wb);
+    if (!rc && b) rc = ensure(c, c->s_b, B * wb);
+    if (!rc) rc = ensure(c, c->s_out, B * wb);
+    if (!rc) rc = ensure(c, c->s_lv1, B * 1025 * sizeof(uint32_t));
+    if (rc) return rc;
+    if (c->s_ties.bytes < B) {
+        rc = ensure(c, c->s_ties, B);
+        if (rc) return rc;
+        HIPCHK(c, hipMemsetAsync(c->s_ties.p, 0, c->s_ties.bytes, c->stream));
+    }
+    if (!c->pipe_ev) HIPCHK(c, hipEventCreateWithFlags(&c->pipe_ev, hipEventDisableTiming));
+    for (hipStream_t &p : c->pipe)
+        if (!p) HIPCHK(c, hipStreamCreateWithFlags(&p, hipStreamNonBlocking));
+    if (!c->workers) c->workers.reset(new WorkerPool(PIPE_STREAMS));
+    // everything enqueued on the context stream (key loads, the flags' memset) first
+    HIPCHK(c, hipEventRecord(c->pipe_ev, c->stream));
+    LaunchOpts o = c->opts;
+    if (!o.br_form) o.br_form = 1;  // whole form for every chunk (a chunk is a quarter round)
+    char *pin_ops = c->pin_in, *pin_a = c->pin_in + ops_bytes, *pin_b = pin_a + a_bytes;
+    uint8_t *d_ops = (uint8_t *)c->s_ops.p;
+    uint32_t *d_a = (uint32_t *)c->s_a.p, *d_b = (uint32_t *)c->s_b.p, *d_out = (uint32_t *)c->s_out.p;
+    uint32_t *d_lv1 = (uint32_t *)c->s_lv1.p;
+    std::vector<hipError_t> err(S, hipSuccess);
+    std::vector<const char *> where(S, "");
+    c->workers->run(S, [&](int s) {
+        hipStream_t st = c->pipe[s];
+        auto chk = [&](hipError_t e, const char *what) {
+            if (e != hipSuccess && err[s] == hipSuccess) {
+                err[s] = e;
+                where[s] = what;
+            }
+            return e == hipSuccess;
+        };
+        if (!chk(hipSetDevice(c->device), "hipSetDevice") || !chk(hipStreamWaitEvent(st, c->pipe_ev, 0), "hipStreamWaitEvent"))
+            return;
+        for (size_t k = (size_t)s; k < nch; k += (size_t)S) {
+            const size_t k0 = k * chunk, n = std::min(B, k0 + chunk) - k0;
+            if (ops) std::memcpy(pin_ops + k0, ops + k0, n);
+            std::memcpy(pin_a + k0 * wb, a + k0 * w, n * wb);
+            if (b) std::memcpy(pin_b + k0 * wb, b + k0 * w, n * wb);
+            if (ops && !chk(hipMemcpyAsync(d_ops + k0, pin_ops + k0, n, hipMemcpyHostToDevice, st), "H2D ops")) return;
+            if (!chk(hipMemcpyAsync(d_a + k0 * w, pin_a + k0 * wb, n * wb, hipMemcpyHostToDevice, st), "H2D a")) return;
+            if (b && !chk(hipMemcpyAsync(d_b + k0 * w, pin_b + k0 * wb, n * wb, hipMemcpyHostToDevice, st), "H2D b"))
+                return;
+            KParams K = c->K;
+            K.tie_flags = (uint8_t *)c->s_ties.p + k0;
+            if (!chk(launch_blind_rotate(K, tables(c), ops ? d_ops + k0 : nullptr, d_a + k0 * w, b ? d_b + k0 * w : nullptr,
+                                         nullptr, tv_dev ? tv_dev : c->d_testvec, c->d_bk, d_lv1 + k0 * 1025, BR_OUT_LV1,
+                                         n, st, o, s == 0 && k == 0 ? &c->last_br : nullptr),
+                     "blind rotation") ||
+                !chk(launch_key_switch(c->K, d_lv1 + k0 * 1025, c->d_ksk, d_out + k0 * w, n, st, c->opts,
+                                       s == 0 && k == 0 ? &c->last_ks : nullptr),
+                     "key switch") ||
+                !chk(hipMemcpyAsync(c->pin_out + k0 * wb, d_out + k0 * w, n * wb, hipMemcpyDeviceToHost, st), "D2H"))
+                return;
+        }
+        if (!chk(hipStreamSynchronize(st), "hipStreamSynchronize")) return;
+        for (size_t k = (size_t)s; k < nch; k += (size_t)S) {
+            const size_t k0 = k * chunk, n = std::min(B, k0 + chunk) - k0;
+            std::memcpy(out + k0 * w, c->pin_out + k0 * wb, n * wb);
+        }
+    });
+    for (int s = 0; s < S; s++)
+        if (err[s] != hipSuccess) {
+            for (int t = 0; t < S; t++) (void)hipStreamSynchronize(c->pipe[t]);
+            return hip_fail(c, err[s], where[s]);
+        }
+    c->bootstraps += B;
+    return sync_check(c);  // the device error word (and the recompute counter) after all streams
+}
+
+// The pipeline serves host-buffer bootstraps of at least one whole-form round
+// (4 x #CUs items) unless TFHE_OPT_HOST_PIPELINE = 0 or device timing is on
+// (its events bracket single launches on the context stream).
+bool use_pipeline(const tfhe_gpu_ctx *c, size_t B) {
+    return c->pipeline && !c->profiling && B >= 4 * device_cus();
+}
+
+}  // namespace
+
+extern "C" {
+
 static int bootstrap_batch_one(tfhe_gpu_ctx *c, const uint32_t *in, uint32_t *out, size_t B) {
     if (!c || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (B == 0) return TFHE_OK;
     HIPCHK(c, hipSetDevice(c->device));
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    if (use_pipeline(c, B)) return pipelined_bootstrap(c, nullptr, in, nullptr, nullptr, out, B);
     const size_t w = tlwe0_words(c);
     int rc = h2d(c, c->s_a, in, B * w * 4);
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
@@ -746,6 +934,8 @@ static int gate_batch_one(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a
     for (size_t i = 0; i < B; i++)
         if (ops[i] > TFHE_GATE_ORYN && ops[i] != TFHE_GATE_COPY) return fail(c, TFHE_ERR_INVALID, "bad gate op");
     HIPCHK(c, hipSetDevice(c->device));
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    if (use_pipeline(c, B)) return pipelined_bootstrap(c, ops, a, b, nullptr, out, B);
     const size_t w = tlwe0_words(c);
     int rc = h2d(c, c->s_ops, ops, B);
     if (!rc) rc = h2d(c, c->s_a, a, B * w * 4);
@@ -781,9 +971,12 @@ static int bootstrap_lut_batch_one(tfhe_gpu_ctx *c, const uint32_t *in, const ui
     if (!c || !testvec || (B && (!in || !out))) return fail(c, TFHE_ERR_INVALID, "null argument");
     if (B == 0) return TFHE_OK;
     HIPCHK(c, hipSetDevice(c->device));
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
     const size_t w = tlwe0_words(c);
-    int rc = h2d(c, c->s_a, in, B * w * 4);
-    if (!rc) rc = h2d(c, c->s_tv, testvec, 2 * c->P.N * 4);
+    int rc = h2d(c, c->s_tv, testvec, 2 * c->P.N * 4);
+    if (rc) return rc;
+    if (use_pipeline(c, B)) return pipelined_bootstrap(c, nullptr, in, nullptr, (const uint32_t *)c->s_tv.p, out, B);
+    rc = h2d(c, c->s_a, in, B * w * 4);
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
     if (!rc)
         rc = run_bootstrap_dev(c, nullptr, (const uint32_t *)c->s_a.p, nullptr, (const uint32_t *)c->s_tv.p,
@@ -1305,6 +1498,7 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     case TFHE_OPT_KS_SEL_ITEMS: ok = v == 8 || v == 16 || v == 32; break;
     case TFHE_OPT_ARITH: ok = v == TFHE_ARITH_AUTO || v == TFHE_ARITH_REFERENCE; break;
     case TFHE_OPT_BR_SPIN_CAP: ok = v >= 0 && v <= 0xFFFFFFFFll; break;
+    case TFHE_OPT_HOST_PIPELINE: ok = v == 0 || v == 1; break;
     case TFHE_OPT_TWIDDLES:
         ok = v == TFHE_TWIDDLES_GLIBC || v == TFHE_TWIDDLES_FDLIBM;
         // tfhe_gpu_keygen transformed the resident BK with the current tables:
@@ -1337,6 +1531,7 @@ int apply_option(tfhe_gpu_ctx *c, int key, int64_t v) {
     case TFHE_OPT_BR_SYNC: o.br_flags = (int)v; break;
     case TFHE_OPT_ARITH: o.arith_strict = v == TFHE_ARITH_REFERENCE; break;
     case TFHE_OPT_BR_SPIN_CAP: c->K.spin_cap = (uint32_t)v; break;
+    case TFHE_OPT_HOST_PIPELINE: c->pipeline = v; break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;
@@ -1373,6 +1568,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_ARITH: *v = o.arith_strict ? TFHE_ARITH_REFERENCE : TFHE_ARITH_AUTO; break;
     case TFHE_OPT_BR_SYNC: *v = o.br_flags; break;
     case TFHE_OPT_BR_SPIN_CAP: *v = c->K.spin_cap; break;
+    case TFHE_OPT_HOST_PIPELINE: *v = c->pipeline; break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;
