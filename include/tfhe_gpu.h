@@ -109,7 +109,9 @@ int         tfhe_gpu_set_stream(tfhe_gpu_ctx *ctx, void *hip_stream);
  * replicates the primary inputs to every device that reads them and places
  * the connected components of the gate DAG (gates joined by gate-to-gate
  * wires) on the devices, largest first onto the least-loaded device, so no
- * gate output crosses a device.  Device-pointer
+ * gate output crosses a device; when one component dominates it splits every
+ * level's gates over the devices instead and all-gathers each level's outputs
+ * (peer copies over xGMI) before the next (TFHE_OPT_CIRCUIT_SPLIT).  Device-pointer
  * (_dev) and stage entry points and the profile timers use the first device.
  * Nothing is exchanged between devices after the key broadcast. */
 int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int *devices, tfhe_gpu_ctx **out);
@@ -145,9 +147,13 @@ enum {
     TFHE_OPT_BR_SPIN_CAP = 11,    /* polls before one slot-counter wait gives up and sets the device
                                      error word (0 = default, 2^22 sleep units; fault-injection tests
                                      set a few polls to see TFHE_ERR_DEVICE come back) */
-    TFHE_OPT_HOST_PIPELINE = 12   /* host-buffer bootstrap / gate / LUT batches of >= 4 x #CUs items:
+    TFHE_OPT_HOST_PIPELINE = 12,  /* host-buffer bootstrap / gate / LUT batches of >= 4 x #CUs items:
                                      1 (default) chunked through pinned staging on 4 streams (copies
                                      overlap the kernels), 0 one H2D -> kernels -> D2H sequence */
+    TFHE_OPT_CIRCUIT_SPLIT = 13   /* multi-device circuit_eval: 0 auto (default: connected components
+                                     on devices, or by levels when one component dominates), 1
+                                     components, 2 levels (each level's gates split over the devices,
+                                     outputs all-gathered by peer copies before the next level) */
 };
 /* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
  * runs fused multiply-adds in the reference's operation order, with a margin

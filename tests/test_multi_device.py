@@ -125,3 +125,64 @@ def test_two_shards_circuit_components(oracle):
     assert [sum(int(b) << i for i, b in enumerate(row)) for row in dec] == [706, 5555]
     single.close()
     multi.close()
+
+
+def test_two_shards_connected_circuit_by_levels(oracle):
+    """SURVEY §8e's level split (TFHE_OPT_CIRCUIT_SPLIT auto): one connected
+    circuit — 2,200 XOR/AND gates over 64 shared inputs, then 2,200 ORs chaining
+    neighbours, so every gate is in one component — is split level by level over
+    two shards, each level's outputs all-gathered before the next.  Both shards
+    run half of every level; the words equal one device's, a sample the oracle's."""
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0, 0])
+    sk = tfhe_amd.SecretKey(single.params, k.k0, k.k1)
+    g = rng(75)
+    n = 2200
+    c = tfhe_amd.Circuit()
+    ins = [c.input() for _ in range(64)]
+    pairs = g.integers(0, 64, (n, 2))
+    l1 = [c.xor(ins[x], ins[y]) if i % 2 else c.and_(ins[x], ins[y]) for i, (x, y) in enumerate(pairs)]
+    l2 = [c.or_(l1[i], l1[(i + 1) % n]) for i in range(n)]
+    c.output(*l2[::7], *l1[:5])
+    bits = g.integers(0, 2, 64).astype(np.uint8)
+    inputs = sk.encrypt_bool(bits, seed0=7500)
+    assert len(set(c.partition(2).tolist())) == 1  # one component
+    before = multi.device_bootstraps()
+    got, depth = c.run(multi, inputs)
+    ran = multi.device_bootstraps() - before
+    want, d1 = c.run(single, inputs)
+    assert depth == d1 == 2 and np.array_equal(got, want)
+    assert ran.sum() == 2 * n and abs(int(ran[0]) - int(ran[1])) <= 2
+    b1 = np.array([(bits[x] ^ bits[y]) if i % 2 else (bits[x] & bits[y]) for i, (x, y) in enumerate(pairs)], bool)
+    b2 = np.array([b1[i] | b1[(i + 1) % n] for i in range(n)], bool)
+    assert np.array_equal(sk.decrypt_bool(got), np.concatenate([b2[::7], b1[:5]]))
+    # forced component placement puts everything on one shard, same words
+    with multi.options(circuit_split=1):
+        before = multi.device_bootstraps()
+        again, _ = c.run(multi, inputs)
+        assert (multi.device_bootstraps() - before).min() == 0
+    assert np.array_equal(again, want)
+    single.close()
+    multi.close()
+
+
+def test_two_shards_adder_forced_level_split(oracle):
+    """The level split on a 33-level adder (levels of 1-32 gates, NOTs none):
+    forced (TFHE_OPT_CIRCUIT_SPLIT = 2), 402 + 304 = 706, words equal one device's."""
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0, 0])
+    sk = tfhe_amd.SecretKey(single.params, k.k0, k.k1)
+    c = tfhe_amd.Circuit()
+    A, Bw = [c.input() for _ in range(16)], [c.input() for _ in range(16)]
+    s, carry = c.ripple_add(A, Bw, c.input())
+    m = c.mux(A[0], carry, Bw[3])  # a NOT inside a level, too
+    c.output(*s, m)
+    bits = [(402 >> i) & 1 for i in range(16)] + [(304 >> i) & 1 for i in range(16)] + [0]
+    inputs = sk.encrypt_bool(bits, seed0=808)
+    with multi.options(circuit_split=2):
+        got, depth = c.run(multi, inputs)
+    want, d1 = c.run(single, inputs)
+    assert depth == d1 and np.array_equal(got, want)
+    assert sum(int(b) << i for i, b in enumerate(sk.decrypt_bool(got[:16]))) == 706
+    single.close()
+    multi.close()

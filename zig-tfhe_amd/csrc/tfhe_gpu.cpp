@@ -119,6 +119,7 @@ struct tfhe_gpu_ctx {
     // kernel-form options (tfhe_gpu_set_option) and what the last launch ran
     LaunchOpts opts{};
     int64_t circuit_pack = 1;
+    int64_t circuit_split = 0;  // TFHE_OPT_CIRCUIT_SPLIT
     int64_t twiddle_source = TFHE_TWIDDLES_GLIBC;
     bool key_from_keygen = false;  // the resident BK was transformed with this context's tables
     uint64_t near_tie_items = 0;   // items the margin guard recomputed (device err[1], read by sync_check)
@@ -1213,10 +1214,80 @@ int tfhe_circuit_schedule(size_t n_inputs, size_t n_gates, const uint8_t *ops, c
     return TFHE_OK;
 }
 
-// The device wire table is laid out in
-// evaluation order — inputs | NOTs of level 0 | gates of level 1 | NOTs of
-// level 1 | ... — so each level's batch writes one contiguous run of slots,
-// and its inputs are gathered by index inside the blind-rotation prologue.
+}  // extern "C"
+
+namespace {
+
+// A circuit's evaluation plan: the level schedule and the device wire table
+// laid out in evaluation order — inputs | NOTs of level 0 | gates of level 1 |
+// NOTs of level 1 | ... — so each level's batch writes one contiguous run of
+// slots; its inputs are gathered by index inside the blind-rotation prologue.
+// idx / cops: per-group gather indices and op codes, concatenated in
+// evaluation order, then the output wires' slots.
+struct CircuitPlan {
+    std::vector<std::vector<uint32_t>> bs, nots;
+    uint32_t max_level = 0;
+    std::vector<uint32_t> idx;
+    std::vector<uint8_t> cops;
+};
+
+const char *plan_circuit(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,
+                         const uint32_t *in_b, size_t n_outputs, const uint32_t *out_wires, bool pack, size_t cus,
+                         CircuitPlan &pl) {
+    const size_t W = n_inputs + n_gates;
+    if (W > 0xFFFFFFFFull) return "too many wires";
+    std::vector<uint32_t> ready;
+    if (const char *why = schedule_levels(n_inputs, n_gates, ops, in_a, in_b, pack, cus, ready, pl.max_level, pl.bs,
+                                          pl.nots))
+        return why;
+    for (size_t o = 0; o < n_outputs; o++)
+        if (out_wires[o] >= W) return "output wire out of range";
+    std::vector<uint32_t> slot(W);
+    for (size_t w = 0; w < n_inputs; w++) slot[w] = (uint32_t)w;
+    uint32_t next = (uint32_t)n_inputs;
+    for (uint32_t lv = 0; lv <= pl.max_level; lv++) {
+        for (uint32_t g : pl.bs[lv]) slot[n_inputs + g] = next++;
+        for (uint32_t g : pl.nots[lv]) slot[n_inputs + g] = next++;
+    }
+    pl.idx.clear();
+    pl.cops.clear();
+    pl.idx.reserve(2 * n_gates + n_outputs);
+    for (uint32_t lv = 0; lv <= pl.max_level; lv++) {
+        for (uint32_t g : pl.bs[lv]) {
+            const bool two = ops[g] <= TFHE_GATE_ORYN;
+            pl.idx.push_back(slot[in_a[g]]);
+            pl.idx.push_back(two ? slot[in_b[g]] : slot[in_a[g]]);
+            pl.cops.push_back(ops[g]);
+        }
+        for (uint32_t g : pl.nots[lv]) pl.idx.push_back(slot[in_a[g]]);
+    }
+    for (size_t o = 0; o < n_outputs; o++) pl.idx.push_back(slot[out_wires[o]]);
+    return nullptr;
+}
+
+// Device side of a plan on one context: wire table with the inputs, the gather
+// indices and op codes, uploaded on its stream.
+int upload_plan(tfhe_gpu_ctx *c, const CircuitPlan &pl, size_t W, size_t n_inputs, const uint32_t *inputs,
+                size_t n_outputs) {
+    const size_t w1 = tlwe0_words(c);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->s_wires, std::max<size_t>(W, 1) * w1 * 4);
+    if (!rc) rc = ensure(c, c->s_cidx, std::max<size_t>(pl.idx.size(), 1) * 4);
+    if (!rc) rc = ensure(c, c->s_cops, std::max<size_t>(pl.cops.size(), 1));
+    if (!rc) rc = ensure(c, c->s_out, std::max<size_t>(n_outputs, 1) * w1 * 4);
+    if (rc) return rc;
+    if (n_inputs) HIPCHK(c, hipMemcpyAsync(c->s_wires.p, inputs, n_inputs * w1 * 4, hipMemcpyHostToDevice, c->stream));
+    if (!pl.idx.empty())
+        HIPCHK(c, hipMemcpyAsync(c->s_cidx.p, pl.idx.data(), pl.idx.size() * 4, hipMemcpyHostToDevice, c->stream));
+    if (!pl.cops.empty())
+        HIPCHK(c, hipMemcpyAsync(c->s_cops.p, pl.cops.data(), pl.cops.size(), hipMemcpyHostToDevice, c->stream));
+    return TFHE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 static int circuit_eval_one(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
                           const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
                           const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels_out) {
@@ -1224,50 +1295,19 @@ static int circuit_eval_one(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *in
         return fail(c, TFHE_ERR_INVALID, "null argument");
     if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
     const size_t W = n_inputs + n_gates, w1 = tlwe0_words(c);
-    if (W > 0xFFFFFFFFull) return fail(c, TFHE_ERR_INVALID, "too many wires");
-    std::vector<uint32_t> ready;
-    std::vector<std::vector<uint32_t>> bs, nots;
-    uint32_t max_level = 0;
     HIPCHK(c, hipSetDevice(c->device));
-    if (const char *why = schedule_levels(n_inputs, n_gates, ops, in_a, in_b, c->circuit_pack != 0,
-                                          device_cus(), ready, max_level, bs, nots))
+    CircuitPlan pl;
+    if (const char *why = plan_circuit(n_inputs, n_gates, ops, in_a, in_b, n_outputs, out_wires, c->circuit_pack != 0,
+                                       device_cus(), pl))
         return fail(c, TFHE_ERR_INVALID, why);
-    for (size_t o = 0; o < n_outputs; o++)
-        if (out_wires[o] >= W) return fail(c, TFHE_ERR_INVALID, "output wire out of range");
-    std::vector<uint32_t> slot(W);
-    for (size_t w = 0; w < n_inputs; w++) slot[w] = (uint32_t)w;
-    uint32_t next = (uint32_t)n_inputs;
-    for (uint32_t lv = 0; lv <= max_level; lv++) {
-        for (uint32_t g : bs[lv]) slot[n_inputs + g] = next++;
-        for (uint32_t g : nots[lv]) slot[n_inputs + g] = next++;
-    }
-    // per-group gather indices and op codes, concatenated in evaluation order
-    std::vector<uint32_t> idx;
-    std::vector<uint8_t> cops;
-    idx.reserve(2 * n_gates + n_outputs);
-    for (uint32_t lv = 0; lv <= max_level; lv++) {
-        for (uint32_t g : bs[lv]) {
-            const bool two = ops[g] <= TFHE_GATE_ORYN;
-            idx.push_back(slot[in_a[g]]);
-            idx.push_back(two ? slot[in_b[g]] : slot[in_a[g]]);
-            cops.push_back(ops[g]);
-        }
-        for (uint32_t g : nots[lv]) idx.push_back(slot[in_a[g]]);
-    }
-    for (size_t o = 0; o < n_outputs; o++) idx.push_back(slot[out_wires[o]]);
-    HIPCHK(c, hipSetDevice(c->device));
-    int rc = ensure(c, c->s_wires, std::max<size_t>(W, 1) * w1 * 4);
-    if (!rc) rc = ensure(c, c->s_cidx, std::max<size_t>(idx.size(), 1) * 4);
-    if (!rc) rc = ensure(c, c->s_cops, std::max<size_t>(cops.size(), 1));
-    if (!rc) rc = ensure(c, c->s_out, std::max<size_t>(n_outputs, 1) * w1 * 4);
+    int rc = upload_plan(c, pl, W, n_inputs, inputs, n_outputs);
     if (rc) return rc;
+    const auto &bs = pl.bs;
+    const auto &nots = pl.nots;
+    const uint32_t max_level = pl.max_level;
     uint32_t *wires = (uint32_t *)c->s_wires.p;
     const uint32_t *d_idx = (const uint32_t *)c->s_cidx.p;
     const uint8_t *d_ops = (const uint8_t *)c->s_cops.p;
-    if (n_inputs) HIPCHK(c, hipMemcpyAsync(wires, inputs, n_inputs * w1 * 4, hipMemcpyHostToDevice, c->stream));
-    if (!idx.empty())
-        HIPCHK(c, hipMemcpyAsync(c->s_cidx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, c->stream));
-    if (!cops.empty()) HIPCHK(c, hipMemcpyAsync(c->s_cops.p, cops.data(), cops.size(), hipMemcpyHostToDevice, c->stream));
     size_t ip = 0, op_pos = 0, sp = n_inputs;
     for (uint32_t lv = 0; lv <= max_level; lv++) {
         const size_t nb = bs[lv].size(), nn = nots[lv].size();
@@ -1499,6 +1539,7 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     case TFHE_OPT_ARITH: ok = v == TFHE_ARITH_AUTO || v == TFHE_ARITH_REFERENCE; break;
     case TFHE_OPT_BR_SPIN_CAP: ok = v >= 0 && v <= 0xFFFFFFFFll; break;
     case TFHE_OPT_HOST_PIPELINE: ok = v == 0 || v == 1; break;
+    case TFHE_OPT_CIRCUIT_SPLIT: ok = v >= 0 && v <= 2; break;
     case TFHE_OPT_TWIDDLES:
         ok = v == TFHE_TWIDDLES_GLIBC || v == TFHE_TWIDDLES_FDLIBM;
         // tfhe_gpu_keygen transformed the resident BK with the current tables:
@@ -1532,6 +1573,7 @@ int apply_option(tfhe_gpu_ctx *c, int key, int64_t v) {
     case TFHE_OPT_ARITH: o.arith_strict = v == TFHE_ARITH_REFERENCE; break;
     case TFHE_OPT_BR_SPIN_CAP: c->K.spin_cap = (uint32_t)v; break;
     case TFHE_OPT_HOST_PIPELINE: c->pipeline = v; break;
+    case TFHE_OPT_CIRCUIT_SPLIT: c->circuit_split = v; break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;
@@ -1569,6 +1611,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_BR_SYNC: *v = o.br_flags; break;
     case TFHE_OPT_BR_SPIN_CAP: *v = c->K.spin_cap; break;
     case TFHE_OPT_HOST_PIPELINE: *v = c->pipeline; break;
+    case TFHE_OPT_CIRCUIT_SPLIT: *v = c->circuit_split; break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;
@@ -1781,6 +1824,125 @@ void partition_gates(size_t n_inputs, size_t n_gates, const uint8_t *ops, const 
     for (size_t g = 0; g < n_gates; g++) dev_of_gate[g] = dev_of_root[dsu.find((uint32_t)g)];
 }
 
+// Level split or components (TFHE_OPT_CIRCUIT_SPLIT: 0 auto, 1 components, 2
+// levels).  Auto: levels when the component placement leaves the busiest device
+// more than 10 % above an even share of at least one whole-form round per device
+// (e.g. one big connected circuit); components otherwise (independent gates,
+// MUXes and adders place evenly, and nothing crosses devices).
+bool split_by_levels(const tfhe_gpu_ctx *c, size_t n_gates, const uint8_t *ops, const std::vector<uint32_t> &dev) {
+    if (c->circuit_split != 0) return c->circuit_split == 2;
+    const size_t D = c->shards.size();
+    std::vector<uint64_t> load(D, 0);
+    uint64_t total = 0;
+    for (size_t g = 0; g < n_gates; g++)
+        if (ops[g] != TFHE_GATE_NOT) {
+            load[dev[g]]++;
+            total++;
+        }
+    const uint64_t even = (total + D - 1) / D;
+    return even >= 4 * device_cus() && *std::max_element(load.begin(), load.end()) * 10 > even * 11;
+}
+
+// circuit_eval over the devices, level by level ("a level barrier
+// across GPUs"), for circuits whose gates form one dominant connected
+// component.  Every device holds the whole wire table in the same layout (the
+// plan of circuit_eval_one, its level packing modelled on all devices' CUs)
+// and the primary inputs.  Per level, device d bootstraps its contiguous slice
+// of the level's gates into its table; each slice is then copied to every other
+// device (peer copies over xGMI, ordered by an event on the producer's stream:
+// an all-gather), and every device applies the level's NOTs itself.  Outputs
+// come from the first device's table.
+int circuit_eval_levels(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates, const uint8_t *ops,
+                        const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs, const uint32_t *out_wires,
+                        uint32_t *outputs, uint32_t *levels_out) {
+    const size_t W = n_inputs + n_gates, D = c->shards.size(), w1 = tlwe0_words(c);
+    CircuitPlan pl;
+    if (const char *why = plan_circuit(n_inputs, n_gates, ops, in_a, in_b, n_outputs, out_wires, c->circuit_pack != 0,
+                                       device_cus() * D, pl))
+        return fail(c, TFHE_ERR_INVALID, why);
+    std::vector<hipEvent_t> ev(D, nullptr);
+    auto cleanup = [&] {
+        for (size_t d = 0; d < D; d++)
+            if (ev[d]) {
+                (void)hipSetDevice(c->shards[d]->device);
+                (void)hipEventDestroy(ev[d]);
+            }
+        (void)hipSetDevice(c->device);
+    };
+    int rc = TFHE_OK;
+    for (size_t d = 0; d < D && !rc; d++) {
+        tfhe_gpu_ctx *s = c->shards[d];
+        rc = upload_plan(s, pl, W, n_inputs, inputs, n_outputs);
+        if (!rc && hipEventCreateWithFlags(&ev[d], hipEventDisableTiming) != hipSuccess) rc = fail(s, TFHE_ERR_HIP, "hipEventCreate");
+        if (rc) rc = fail(c, rc, "device " + std::to_string(s->device) + ": " + s->err);
+    }
+    size_t ip = 0, op_pos = 0, sp = n_inputs;
+    for (uint32_t lv = 0; lv <= pl.max_level && !rc; lv++) {
+        const size_t nb = pl.bs[lv].size(), nn = pl.nots[lv].size(), per = (nb + D - 1) / D;
+        if (nb) {
+            for (size_t d = 0; d < D && !rc; d++) {  // each device its slice
+                tfhe_gpu_ctx *s = c->shards[d];
+                const size_t lo = std::min(nb, d * per), n = std::min(nb, lo + per) - lo;
+                if (!n) continue;
+                if (hipSetDevice(s->device) != hipSuccess) { rc = fail(c, TFHE_ERR_HIP, "hipSetDevice"); break; }
+                uint32_t *wires = (uint32_t *)s->s_wires.p;
+                rc = run_bootstrap_dev(s, (const uint8_t *)s->s_cops.p + op_pos + lo, wires, wires, nullptr,
+                                       wires + (sp + lo) * w1, n, RUN_BOOTSTRAP, (const uint32_t *)s->s_cidx.p + ip + 2 * lo);
+                if (!rc && hipEventRecord(ev[d], s->stream) != hipSuccess) rc = fail(s, TFHE_ERR_HIP, "hipEventRecord");
+                if (rc) rc = fail(c, rc, "device " + std::to_string(s->device) + ": " + s->err);
+            }
+            for (size_t e = 0; e < D && !rc; e++) {  // all-gather of the level's outputs
+                tfhe_gpu_ctx *t = c->shards[e];
+                if (hipSetDevice(t->device) != hipSuccess) { rc = fail(c, TFHE_ERR_HIP, "hipSetDevice"); break; }
+                for (size_t d = 0; d < D && !rc; d++) {
+                    const size_t lo = std::min(nb, d * per), n = std::min(nb, lo + per) - lo;
+                    if (d == e || !n) continue;
+                    tfhe_gpu_ctx *s = c->shards[d];
+                    const size_t off = (sp + lo) * w1;
+                    if (hipStreamWaitEvent(t->stream, ev[d], 0) != hipSuccess ||
+                        hipMemcpyPeerAsync((uint32_t *)t->s_wires.p + off, t->device, (const uint32_t *)s->s_wires.p + off,
+                                           s->device, n * w1 * 4, t->stream) != hipSuccess)
+                        rc = fail(c, TFHE_ERR_HIP, "level all-gather to device " + std::to_string(t->device));
+                }
+            }
+            ip += 2 * nb;
+            op_pos += nb;
+            sp += nb;
+        }
+        if (nn && !rc) {
+            for (size_t d = 0; d < D && !rc; d++) {  // every device negates the level's NOT inputs itself
+                tfhe_gpu_ctx *s = c->shards[d];
+                uint32_t *wires = (uint32_t *)s->s_wires.p;
+                if (hipSetDevice(s->device) != hipSuccess ||
+                    launch_tlwe_gather(s->K, wires, (const uint32_t *)s->s_cidx.p + ip, wires + sp * w1, nn, true,
+                                       s->stream) != hipSuccess)
+                    rc = fail(c, TFHE_ERR_HIP, "NOT gather on device " + std::to_string(s->device));
+            }
+            ip += nn;
+            sp += nn;
+        }
+    }
+    for (size_t d = 1; d < D && !rc; d++) {  // every device's work done, its error word clean
+        tfhe_gpu_ctx *s = c->shards[d];
+        if (hipSetDevice(s->device) != hipSuccess) { rc = fail(c, TFHE_ERR_HIP, "hipSetDevice"); break; }
+        rc = sync_check(s);
+        if (rc) rc = fail(c, rc, "device " + std::to_string(s->device) + ": " + s->err);
+    }
+    if (!rc && hipSetDevice(c->device) != hipSuccess) rc = fail(c, TFHE_ERR_HIP, "hipSetDevice");
+    if (!rc && n_outputs) {
+        if (launch_tlwe_gather(c->K, (const uint32_t *)c->s_wires.p, (const uint32_t *)c->s_cidx.p + ip,
+                               (uint32_t *)c->s_out.p, n_outputs, false, c->stream) != hipSuccess)
+            rc = fail(c, TFHE_ERR_HIP, "output gather");
+        else
+            rc = d2h_sync(c, outputs, c->s_out.p, n_outputs * w1 * 4);
+    } else if (!rc) {
+        rc = sync_check(c);
+    }
+    cleanup();
+    if (!rc && levels_out) *levels_out = pl.max_level;
+    return rc;
+}
+
 // circuit_eval over the devices.  Primary inputs are read-only, so every
 // device gets its own copy of the ones it reads; only gate-to-gate wires tie
 // gates together.  The connected components of the gate DAG under those wires
@@ -1804,6 +1966,8 @@ int circuit_eval_multi(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs,
     }
     std::vector<uint32_t> dev_of_gate;
     partition_gates(n_inputs, n_gates, ops, in_a, in_b, D, dev_of_gate);
+    if (split_by_levels(c, n_gates, ops, dev_of_gate))
+        return circuit_eval_levels(c, n_inputs, inputs, n_gates, ops, in_a, in_b, n_outputs, out_wires, outputs, levels_out);
     // per-device sub-circuits; wires renumbered: the device's inputs first, then its gates
     struct Sub {
         std::vector<uint32_t> inputs, in_a, in_b, out_wires, out_index;
