@@ -528,6 +528,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
+    ties0 = ctx.near_tie_items()
     ctx.profile_begin()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -536,7 +537,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    br_ms, ks_ms, launches = ctx.profile_end()
+    br_ms, ks_ms, launches = ctx.profile_end()  # synchronises: the device error word and the guard's counter
+    recomputed = ctx.near_tie_items() - ties0
 
     stats = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device=device)
     if world > 1:
@@ -561,6 +563,9 @@ def main():
             "roofline": roof,
             "roofline_hbm_accounting": hbm,
             "key_switch": {"kernel": kernels.split(" + ")[-1], "avg_ms": round(ks_avg_s * 1e3, 3)},
+            "margin_guard": {"recomputed_items": recomputed, "items": B * args.steps,
+                             "note": "fused arithmetic; items rounding within 1/8 of a tie are redone in the "
+                                     "reference's expression trees inside the timed launches (DESIGN.md §6.1)"},
             "kernel_build_id": kernel_build_id(),
             "kernel_source_sha256": kernel_source_hash(),
             "decrypt_check": all_correct,
