@@ -129,7 +129,8 @@ int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
  * fastest forms).  Set on a context before use; a multi-device context
  * passes them to every device.  TFHE_ERR_INVALID for an unknown key or value. */
 enum {
-    TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 2 split, 3 latency, 4 pair */
+    TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 2 split, 3 latency, 4 pair,
+                                     5 octo (8 items per workgroup, two gate waves per SIMD) */
     TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
     TFHE_OPT_KS_FORM = 3,         /* key switch: 0 lanes (default), 1 select / gather */
     TFHE_OPT_KS_NARROW = 4,       /* basebit 2: 0 auto (default), 1 32-word x 4-wave blocks */

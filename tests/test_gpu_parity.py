@@ -94,7 +94,8 @@ def test_key_switch_vs_oracle(oracle, pname, B, form):
 
 # ---- blind rotation / bootstrap ---------------------------------------------
 @pytest.mark.parametrize("form", ["whole", "whole-noloader", "whole-reference", "whole-noloader-reference",
-                                  "whole-barrier", "whole-barrier-reference", "split", "wide", "pair", "pair-reference"])
+                                  "whole-barrier", "whole-barrier-reference", "split", "wide", "pair", "pair-reference",
+                                  "octo", "octo-reference"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
 def test_blind_rotate_vs_oracle(oracle, pname, B, form):
     """All kernel forms (1 wave per item with or without loader waves, fused or
@@ -112,23 +113,26 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
             assert c.last_kernels().endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
         if form.startswith("pair"):  # L = 1 (UINT4) runs the pair form in the reference's trees too
             assert c.last_kernels().startswith("k_blind_rotate_pair<") == (pname == "uint4" or form == "pair")
-        prefix = {"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<", "wide": "k_blind_rotate_wide<"}
+        prefix = {"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<", "wide": "k_blind_rotate_wide<",
+                  "octo": "k_blind_rotate_octo<"}
         if form.split("-")[0] in prefix:
             assert c.last_kernels().startswith(prefix[form.split("-")[0]])
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
-@pytest.mark.parametrize("form,loader,sync", [("whole", 1, 1), ("whole", 1, 0), ("whole", 0, 0), ("pair", 1, 0)])
+@pytest.mark.parametrize("form,loader,sync", [("whole", 1, 1), ("whole", 1, 0), ("whole", 0, 0), ("pair", 1, 0),
+                                              ("octo", 1, 0)])
 def test_whole_form_every_idle_slot_count(oracle, form, loader, sync):
     """Whole form at B = 1..8: the last workgroup has 3, 2, 1 or 0 idle gate slots
     (clamped copies of the last item: they read in bounds, follow the barrier
-    schedule and store nothing).  Regression for the round-1 development fault in
+    schedule and store nothing); the octo form (8 items per workgroup) at B = 1..9
+    has 7..0 idle slots.  Regression for the round-1 development fault in
     test_blind_rotate_vs_oracle[80-3-whole]."""
     c, k = ctx_for(oracle, "80")
-    cts = u32rand(rng(17), 8, k.p.n + 1)
+    cts = u32rand(rng(17), 9, k.p.n + 1)
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
     with c.options(br_form=form, br_loader=loader, br_sync=sync):
-        for B in range(1, 9):
+        for B in range(1, 10 if form == "octo" else 9):
             assert np.array_equal(c.blind_rotate_batch(cts[:B]), want[:B]), B
 
 
@@ -518,7 +522,7 @@ def test_slot_counters_and_barrier_agree_at_full_size(oracle):
         assert np.array_equal(sk.decrypt_bool(flags), ~(a_bits.astype(bool) & b_bits.astype(bool)))
 
 
-@pytest.mark.parametrize("form", ["auto", "whole", "split", "pair", "wide"])
+@pytest.mark.parametrize("form", ["auto", "whole", "split", "pair", "wide", "octo"])
 def test_margin_guard_recomputes_near_ties(oracle, form):
     """under a crafted key (conftest.crafted_near_tie_case) the
     unguarded fused arithmetic parts from the reference (the oracle's fused mode

@@ -217,6 +217,23 @@ struct LdsTw {
     DEV void pass_c(C2 *w, int t) const { tw_pass_c(w, tw, t); }
 };
 
+// LdsTw whose table reads stay at their pass (an opaque pointer per read): with
+// many transforms per step hipcc otherwise hoists the loop-invariant twiddles of
+// passes B and C out of the step loop, 56 VGPRs held for the whole launch (the
+// octo form spilled).
+struct LdsTwAtPass : LdsTw {
+    DEV void pass_b(C2 *w, int t) const {
+        const C2 *p = tw;
+        asm volatile("" : "+v"(p));
+        tw_pass_b(w, p, t);
+    }
+    DEV void pass_c(C2 *w, int t) const {
+        const C2 *p = tw;
+        asm volatile("" : "+v"(p));
+        tw_pass_c(w, p, t);
+    }
+};
+
 // Pass A: stages len = 2, 4, 8 (bits 0-2 of the bit-reversed position are the
 // register index q).
 template <bool INV, bool FU = false>
@@ -321,12 +338,14 @@ DEV void ex2_regs(C2 *d) {
     swap_lane_reg<0>(d[0], d[1]); swap_lane_reg<0>(d[2], d[3]); swap_lane_reg<0>(d[4], d[5]); swap_lane_reg<0>(d[6], d[7]);
 }
 
-template <int NF>
+template <int NF, bool LDS = false>
 DEV void exchange2(C2 (*d)[8], C2 *xb, int t) {
 #ifndef TFHE_EX2_LDS
+    if (!LDS) {
 #pragma unroll
-    for (int f = 0; f < NF; f++) ex2_regs(d[f]);
-    return;
+        for (int f = 0; f < NF; f++) ex2_regs(d[f]);
+        return;
+    }
 #endif
     int wb = (t & 7) + 64 * (t >> 3);
 #pragma unroll
@@ -410,7 +429,7 @@ DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
 #endif
 }
 
-template <int NF, bool INV, bool FU = false, class TW>
+template <int NF, bool INV, bool FU = false, class TW, bool EX2LDS = false>
 DEV void fft512(C2 (*d)[8], C2 *xb, const TW &T, int t) {
 #pragma unroll
     for (int f = 0; f < NF; f++) passA<INV, FU>(d[f], T.a);
@@ -421,7 +440,7 @@ DEV void fft512(C2 (*d)[8], C2 *xb, const TW &T, int t) {
 #pragma unroll
         for (int f = 0; f < NF; f++) passBC<INV, FU>(d[f], w);
     }
-    exchange2<NF>(d, xb, t);
+    exchange2<NF, EX2LDS>(d, xb, t);
     {
         C2 w[7];
         T.pass_c(w, t);
@@ -1192,6 +1211,222 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     } else {
         uint32_t *o = out + g * (size_t)2048;
         for (int j = t; j < 2048; j += 64) o[j] = s_acc[j];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Blind rotation, "octo" form (large batches): EIGHT items per 512-thread
+// workgroup, one wave each, so every SIMD runs two gate waves that both issue
+// f64 work (the whole form: one gate wave + one loader wave per SIMD).  The 8
+// gates share each BK row pair brought into LDS by one DMA (twice the reuse of
+// the whole form).  LDS per gate is ONE 8 KB buffer: it holds the accumulator
+// between steps (the rotation gather reads it), and once the gather has
+// produced tmp = X^a~ acc - acc + offset in registers (kept there for all 2L
+// rows' digits) it is the gate's FFT exchange buffer until the accumulator is
+// written back.  BK 2 x 32 KB + tables 16 KB + 8 x 8 KB + a~ 8 x 2 KB = 160 KB.
+// No loader waves (a third wave per SIMD does not fit the VGPR file): every
+// thread issues 4 x 16 B of each pair's DMA, and one workgroup barrier per row
+// pair publishes the pair's slot and retires the other (as the whole form's
+// non-loader variant).  Same arithmetic and row order as the whole form.
+// ---------------------------------------------------------------------------
+constexpr int BO_GATES = 8;
+constexpr int BO_LDS_BUF = 2048 * 4;  // per gate: accumulator / exchange buffer
+constexpr int BO_LDS_AT = 1024 * 2;   // per gate
+constexpr int BO_LDS_TOTAL = BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST + BO_GATES * (BO_LDS_BUF + BO_LDS_AT);
+static_assert(BO_LDS_TOTAL <= 160 * 1024, "octo form LDS");
+
+// LDS-DMA of one BK row pair (32 KB) into a slot by 512 threads: 4 x 16 B each,
+// in the scalar-base form (SGPR pair address + the thread's 32-bit byte
+// offset): no 64-bit per-lane addresses to keep live across the unrolled rows.
+DEV void issue_bk_pair_async512(const double2 *__restrict__ src, double2 *slot, int tid) {
+    const uint32_t base = (uint32_t)(size_t)(lds_void_t *)slot + (uint32_t)(tid & ~63) * 16;
+    const uint32_t voff = (uint32_t)tid * 16;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(base + 512 * 16 * k);
+        const double2 *piece = src + 512 * k;
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(dst), "s"(piece)
+            : "memory");
+    }
+}
+
+// Digits of row `row` (runtime) from the tmp words in registers (lane word m =
+// coefficient t + 64m), twist factors from the LDS table.
+template <bool FU>
+DEV void load_digits_row_regs(C2 *d, const uint32_t *tA, const uint32_t *tB, int row, int L, int bgbit,
+                              const C2 *twist_t) {
+    const bool from_a = row < L;
+    const int level = from_a ? row : row - L;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int m = br3(q);
+        const uint32_t x0 = from_a ? tA[m] : tB[m], x1 = from_a ? tA[m + 8] : tB[m + 8];
+        d[q] = twist_in<FU>(digit_f64(x0, level, bgbit), digit_f64(x1, level, bgbit), twist_t[64 * m]);
+    }
+}
+
+// MAC of one row (fmaInFd1024's row term for both outputs) from LDS, the BK
+// words of frequency group q+1 read while group q's flops issue.
+template <bool FU>
+DEV void mac_row_lds(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t) {
+    double2 k[2][2];
+    k[0][0] = bk[t];
+    k[0][1] = bk[64 + t];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int c = q & 1;
+        if (q + 1 < 8) {
+            k[c ^ 1][0] = bk[(2 * q + 2) * 64 + t];
+            k[c ^ 1][1] = bk[(2 * q + 3) * 64 + t];
+        }
+        const C2 x = d[q];
+        const double2 ka = k[c][0], kb = k[c][1];
+        if (FU) {
+            fa[q] = c2(fmad(x.x, ka.x, fmad(-x.y, ka.y, fa[q].x)), fmad(x.x, ka.y, fmad(x.y, ka.x, fa[q].y)));
+            fb[q] = c2(fmad(x.x, kb.x, fmad(-x.y, kb.y, fb[q].x)), fmad(x.x, kb.y, fmad(x.y, kb.x, fb[q].y)));
+        } else {
+            const C2 ta = c2(x.x * ka.x - x.y * ka.y, x.x * ka.y + x.y * ka.x);
+            const C2 tb = c2(x.x * kb.x - x.y * kb.y, x.x * kb.y + x.y * kb.x);
+            fa[q] = c2(fa[q].x + ta.x, fa[q].y + ta.y);
+            fb[q] = c2(fb[q].x + tb.x, fb[q].y + tb.y);
+        }
+    }
+}
+
+// The 2L rows of one CMUX step in the octo form, in the reference's row order
+// (rolled: unrolled, hipcc keeps every row's LDS addresses and spills): per row
+// the digits, one forward transform (both exchanges through the gate's buffer:
+// the partner wave on the SIMD covers their latency), at the first row of a
+// pair the pair's barrier (its slot published, the other retired) and the next
+// pair's DMA into the other slot, then the row's MAC.  Pair k0 + r/2.
+template <int L, bool FU>
+DEV void octo_rows(const uint32_t *tA, const uint32_t *tB, int bgbit, const LdsTwAtPass &T, const C2 *twist_t,
+                   C2 *xb, int t, int tid, C2 *fa, C2 *fb, double2 *s_bk, uint32_t k0,
+                   const double2 *__restrict__ bkd, uint32_t pairs) {
+#pragma unroll 1
+    for (int r = 0; r < 2 * L; r++) {
+        const uint32_t k = k0 + (uint32_t)(r >> 1);
+        C2 d[1][8];
+        load_digits_row_regs<FU>(d[0], tA, tB, r, L, bgbit, twist_t);
+#ifndef TFHE_KO_FFT
+        fft512<1, false, FU, LdsTwAtPass, true>(d, xb, T, t);
+#endif
+        if ((r & 1) == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's pieces of pair k landed
+            __syncthreads();  // pair k in slot k & 1 for every wave; every wave done with pair k - 1
+            if (k + 1 < pairs)
+                issue_bk_pair_async512(bkd + (size_t)((k + 1) / L) * L * 2048 + (size_t)((k + 1) % L) * 2048,
+                                       s_bk + ((k + 1) & 1) * 2048, tid);
+        }
+        mac_row_lds<FU>(fa, fb, d[0], s_bk + (k & 1) * 2048 + (r & 1) * 1024, t);
+    }
+}
+
+template <int L, bool SMALL, bool FU>
+__global__ __launch_bounds__(512, 1) void k_blind_rotate_octo(
+    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
+    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[BO_LDS_TOTAL];
+    const int tid = threadIdx.x;
+    const int t = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    double2 *s_bk = reinterpret_cast<double2 *>(smem);
+    C2 *s_tw = reinterpret_cast<C2 *>(smem + BR_LDS_BK);
+    C2 *s_twist = reinterpret_cast<C2 *>(smem + BR_LDS_BK + BR_LDS_TW);
+    unsigned char *gbase = smem + BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;
+    uint32_t *s_buf = reinterpret_cast<uint32_t *>(gbase + w * BO_LDS_BUF);
+    C2 *s_x = reinterpret_cast<C2 *>(s_buf);
+    uint16_t *s_at = reinterpret_cast<uint16_t *>(gbase + BO_GATES * BO_LDS_BUF + w * BO_LDS_AT);
+
+    const int n = P.n;
+    const size_t g_raw = (size_t)blockIdx.x * BO_GATES + w;
+    const bool valid = g_raw < B;
+    const size_t g = valid ? g_raw : B - 1;  // ragged tail: compute a copy, store nothing
+    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
+    const uint32_t *A = in_a + ia * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
+    const int op = ops ? (int)ops[g] : 255;
+    const uint32_t pairs = (uint32_t)n * L;
+
+    issue_bk_pair_async512(bkd, s_bk, tid);  // pair 0 into slot 0, lands under the prologue
+    for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
+    int bt = 0;  // a~_i, b~ (trgsw.zig:297, :312), 64-bit adds
+    for (int i = t; i <= n; i += 64) {
+        const uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
+        const uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
+        if (i < n) s_at[i] = (uint16_t)tl;
+        else bt = 2048 - (int)tl;
+    }
+    bt = __builtin_amdgcn_readlane(bt, n & 63);
+    uint32_t accA[16], accB[16];  // acc = X^{b~} * testvec (trgsw.zig:300-306)
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        accA[m] = rot_read(testvec, t + 64 * m, bt);
+        accB[m] = rot_read(testvec + 1024, t + 64 * m, bt);
+        s_buf[t + 64 * m] = accA[m];
+        s_buf[1024 + t + 64 * m] = accB[m];
+    }
+    __syncthreads();  // tables visible to every wave
+    LdsTwAtPass T;
+    T.init(s_tw, TT);
+    const C2 *twist_t = s_twist + t;
+    int at_next = s_at[0];
+    uint32_t near = NEAR_NONE;
+
+    for (int i = 0; i < n; i++) {
+        const int at = __builtin_amdgcn_readfirstlane(at_next);
+        at_next = s_at[i + 1 < n ? i + 1 : i];
+        // tmp = X^{a~} acc - acc + offset, kept in registers for every row's digits
+        uint32_t tA[16], tB[16];
+        const int rb = (t - at) & 2047;
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            const int j = (rb + 64 * m) & 1023;
+            tA[m] = s_buf[j];
+            tB[m] = s_buf[1024 + j];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            const bool neg = ((rb + 64 * m) & 1024) != 0;  // X^a~ wraps past N: negacyclic sign
+            tA[m] = (neg ? 0u - tA[m] : tA[m]) - accA[m] + P.offset;
+            tB[m] = (neg ? 0u - tB[m] : tB[m]) - accB[m] + P.offset;
+        }
+        wave_sync();  // the gather's reads precede the exchanges' writes into the buffer
+        C2 fa[8], fb[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0
+            fa[q] = c2(0.0, 0.0);
+            fb[q] = c2(0.0, 0.0);
+        }
+        octo_rows<L, FU>(tA, tB, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (uint32_t)(L * i), bkd, pairs);
+        inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB, near);
+        wave_sync();
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            s_buf[t + 64 * m] = accA[m];
+            s_buf[1024 + t + 64 * m] = accB[m];
+        }
+        wave_sync();
+    }
+    if (FU) near_tie_flag(P, near, g, valid);
+
+    if (!valid) return;
+    if (out_mode == BR_OUT_LV1) {  // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
+        uint32_t *o = out + g * (size_t)1025;
+        for (int j = t; j <= 1024; j += 64) o[j] = j == 0 ? s_buf[0] : j < 1024 ? 0u - s_buf[1024 - j] : s_buf[1024];
+    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {  // sampleExtractIndex2 (trlwe.zig:165-180)
+        uint32_t *o = out + g * (size_t)(n + 1);
+        for (int j = t; j <= n; j += 64) o[j] = j == 0 ? s_buf[0] : j < n ? 0u - s_buf[n - j] : s_buf[1024];
+    } else {
+        uint32_t *o = out + g * (size_t)2048;
+        for (int j = t; j < 2048; j += 64) o[j] = s_buf[j];
     }
 }
 
@@ -2380,6 +2615,29 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     // fused arithmetic in the exact-integer regime (SMALL) unless the
     // reference expression trees are requested (TFHE_OPT_ARITH)
     const bool fused = small && O.arith_strict == 0;
+    if (form == 'o') {  // octo form: 8 items per workgroup, two gate waves per SIMD
+        const dim3 grid((unsigned)((B + BO_GATES - 1) / BO_GATES)), block(64 * BO_GATES);
+#define BO_LAUNCH(L_, S_)                                                                                            \
+        do {                                                                                                         \
+            if (fused) {                                                                                             \
+                hipLaunchKernelGGL((k_blind_rotate_octo<L_, S_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, \
+                                   testvec, bk2, out, out_mode, B);                                                  \
+                if (used) *used = "k_blind_rotate_octo<" #L_ "," #S_ ",true> (octo form, fused)";                    \
+            } else {                                                                                                 \
+                hipLaunchKernelGGL((k_blind_rotate_octo<L_, S_, false>), grid, block, 0, s, P, T, ops, in_a, in_b,   \
+                                   idx, testvec, bk2, out, out_mode, B);                                             \
+                if (used) *used = "k_blind_rotate_octo<" #L_ "," #S_ ",false> (octo form)";                          \
+            }                                                                                                        \
+        } while (0)
+        switch (P.L) {
+        case 1: if (small) BO_LAUNCH(1, true); else BO_LAUNCH(1, false); break;
+        case 2: if (small) BO_LAUNCH(2, true); else BO_LAUNCH(2, false); break;
+        case 3: if (small) BO_LAUNCH(3, true); else BO_LAUNCH(3, false); break;
+        default: return hipErrorInvalidValue;
+        }
+#undef BO_LAUNCH
+        return hipGetLastError();
+    }
     if (form == 'p') {  // pair form (2 waves per item); falls back to the whole form where not exact
         bool ok = false;
         switch (P.L) {
@@ -2496,7 +2754,7 @@ static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T
                                             const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
                                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (O.br_form) {  // forced form (TFHE_OPT_BR_FORM): the whole batch in one launch
-        const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : 'w';
+        const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : O.br_form == 5 ? 'o' : 'w';
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
     if (B <= BR_WIDE_MAX_ITEMS)
