@@ -149,8 +149,9 @@ enum {
                                      error word (0 = default, 2^22 sleep units; fault-injection tests
                                      set a few polls to see TFHE_ERR_DEVICE come back) */
     TFHE_OPT_HOST_PIPELINE = 12,  /* host-buffer bootstrap / gate / LUT batches of >= 4 x #CUs items:
-                                     1 (default) chunked through pinned staging on 4 streams (copies
-                                     overlap the kernels), 0 one H2D -> kernels -> D2H sequence */
+                                     0 (default) one H2D -> kernels -> D2H sequence, 1 chunked through
+                                     pinned staging on 4 streams (measured slower on the MI355X box,
+                                     whose pageable copies run at ~50 GB/s: DESIGN.md §2.1) */
     TFHE_OPT_CIRCUIT_SPLIT = 13   /* multi-device circuit_eval: 0 auto (default: connected components
                                      on devices, or by levels when one component dominates), 1
                                      components, 2 levels (each level's gates split over the devices,

@@ -226,7 +226,7 @@ def test_gate_batch_rounds_and_tail(oracle, loader):
     b_bits = g.integers(0, 2, n).astype(np.uint8)
     A = sk.encrypt_bool(a_bits, seed0=31_000)
     B = sk.encrypt_bool(b_bits, seed0=41_000)
-    with c.options(br_loader=loader, host_pipeline=0):
+    with c.options(br_loader=loader):
         out = c.gate_batch(ops, A, B)
     ab, bb = a_bits.astype(bool), b_bits.astype(bool)
     want_bits = np.zeros(n, bool)
@@ -237,9 +237,9 @@ def test_gate_batch_rounds_and_tail(oracle, loader):
     idx = np.array([0, 1023, 1024, 2047, 2048, n - 1])
     want = oracle.gate_batch(k.p, ops[idx], A[idx], B[idx], k.ck, threads=6)
     assert np.array_equal(out[idx], want)
-    # the host-buffer pipeline (default above one round: 256-item chunks on 4 streams
+    # the host-buffer pipeline (TFHE_OPT_HOST_PIPELINE: 256-item chunks on 4 streams
     # through pinned staging) gives the same words
-    with c.options(br_loader=loader):
+    with c.options(br_loader=loader, host_pipeline=1):
         assert np.array_equal(c.gate_batch(ops, A, B), out)
 
 

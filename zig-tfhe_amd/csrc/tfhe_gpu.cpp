@@ -138,7 +138,7 @@ struct tfhe_gpu_ctx {
     char *pin_in = nullptr, *pin_out = nullptr;
     size_t pin_in_bytes = 0, pin_out_bytes = 0;
     std::unique_ptr<WorkerPool> workers;
-    int64_t pipeline = 1;  // TFHE_OPT_HOST_PIPELINE
+    int64_t pipeline = 0;  // TFHE_OPT_HOST_PIPELINE (off by default: measured slower)
     std::vector<ncclComm_t> comms;   // one communicator per shard, created on the first key broadcast
 };
 

@@ -673,17 +673,30 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
 #ifndef TFHE_KO_INV
     fft512_x2<true, ONEBUF, FU>(e, xb, T, t);
 #endif
+#ifdef TFHE_GUARD_CHAINS
+    uint32_t nq[4] = {NEAR_NONE, NEAR_NONE, NEAR_NONE, NEAR_NONE};
+#endif
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         double ra, ia, rb, ib;
         const C2 w = tws[q * TS];
         untwist_out<false, FU>(e[0][q], w, ra, ia);
         untwist_out<false, FU>(e[1][q], w, rb, ib);
+#ifdef TFHE_GUARD_CHAINS  // A/B: four independent near-tie accumulators, joined at the end
+        accA[q] += to_torus<SMALL, FU>(ra, nq[0]);
+        accA[q + 8] += to_torus<SMALL, FU>(ia, nq[1]);
+        accB[q] += to_torus<SMALL, FU>(rb, nq[2]);
+        accB[q + 8] += to_torus<SMALL, FU>(ib, nq[3]);
+#else
         accA[q] += to_torus<SMALL, FU>(ra, near);
         accA[q + 8] += to_torus<SMALL, FU>(ia, near);
         accB[q] += to_torus<SMALL, FU>(rb, near);
         accB[q + 8] += to_torus<SMALL, FU>(ib, near);
+#endif
     }
+#ifdef TFHE_GUARD_CHAINS
+    near = min(near, min(min(nq[0], nq[1]), min(nq[2], nq[3])));
+#endif
 }
 
 // Forward transforms + MAC of row pair (2RP, 2RP+1) against `bk` (the pair's

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "9eb2c2abe875f7dc"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "af1aa8960787e960"; }

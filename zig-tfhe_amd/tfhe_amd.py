@@ -27,7 +27,7 @@ OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_
            "circuit_split": 13}
 OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 0, "ks_narrow": 0, "ks_item_groups": 0,
                    "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1, "br_spin_cap": 0,
-                   "host_pipeline": 1, "circuit_split": 0}
+                   "host_pipeline": 0, "circuit_split": 0}
 # status codes (include/tfhe_gpu.h TFHE_ERR_*)
 ERR_INVALID, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_IO, ERR_DEVICE = -1, -2, -3, -4, -5, -6
 BR_FORMS = {"auto": 0, "whole": 1, "split": 2, "wide": 3, "pair": 4, "octo": 5}
