@@ -309,6 +309,31 @@ def test_lut_config5_full_4096_uint4(oracle):
     assert np.array_equal(out[idx], want)
 
 
+@pytest.mark.parametrize("extra", [0, 300, 1500])
+def test_lut_uint4_octo_rounds_and_tails(oracle, extra):
+    """L = 1 dispatch (launch_blind_rotate_forms): full octo rounds (8 items x
+    #CUs) then the rest by the whole / latency policy (extra 300: latency-form
+    tail; 1,500: one whole-form round + a latency-form tail).  Bit-identical to
+    the forced whole form, and to the oracle at the range boundaries."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    c, k = ctx_for(oracle, "uint4")
+    B = 8 * cus + extra
+    tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (3 * x + 1) % 16)
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    msgs = rng(B).integers(0, 16, B).astype(np.uint32)
+    cts = sk.encrypt_lwe_message(msgs, 16, seed0=B)
+    out = c.bootstrap_lut_batch(cts, tv)
+    assert c.last_kernels().startswith("k_blind_rotate_octo<1,")
+    with c.options(br_form="whole"):
+        assert np.array_equal(c.bootstrap_lut_batch(cts, tv), out)
+    assert np.array_equal(sk.decrypt_lwe_message(out, 16), (3 * msgs + 1) % 16)
+    idx = sorted({0, 8 * cus - 1, min(8 * cus, B - 1), min(8 * cus + 1024, B - 1), B - 1})
+    want = oracle.gate_batch(k.p, np.full(len(idx), 255, np.uint8), cts[idx], cts[idx], k.ck, testvec=tv,
+                             threads=len(idx))
+    assert np.array_equal(out[idx], want)
+
+
 def test_lut_uint4_golden_fixture(oracle):
     """The committed config-5 fixture (tests/golden/lut_uint4.npz) through
     tfhe_gpu_bootstrap_lut_batch with the oracle's seeded UINT4 key: bit-identical."""

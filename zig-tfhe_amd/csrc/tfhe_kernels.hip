@@ -673,30 +673,22 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
 #ifndef TFHE_KO_INV
     fft512_x2<true, ONEBUF, FU>(e, xb, T, t);
 #endif
-#ifdef TFHE_GUARD_CHAINS
+    // four independent near-tie accumulators, joined at the end: one min chain
+    // would serialise 32 dependent v_min per call (A/B, profiles/r03e_guard_chains_lut_octo.txt:
+    // guard cost 0.8 % with four chains, 2.2 % with one)
     uint32_t nq[4] = {NEAR_NONE, NEAR_NONE, NEAR_NONE, NEAR_NONE};
-#endif
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         double ra, ia, rb, ib;
         const C2 w = tws[q * TS];
         untwist_out<false, FU>(e[0][q], w, ra, ia);
         untwist_out<false, FU>(e[1][q], w, rb, ib);
-#ifdef TFHE_GUARD_CHAINS  // A/B: four independent near-tie accumulators, joined at the end
         accA[q] += to_torus<SMALL, FU>(ra, nq[0]);
         accA[q + 8] += to_torus<SMALL, FU>(ia, nq[1]);
         accB[q] += to_torus<SMALL, FU>(rb, nq[2]);
         accB[q + 8] += to_torus<SMALL, FU>(ib, nq[3]);
-#else
-        accA[q] += to_torus<SMALL, FU>(ra, near);
-        accA[q + 8] += to_torus<SMALL, FU>(ia, near);
-        accB[q] += to_torus<SMALL, FU>(rb, near);
-        accB[q + 8] += to_torus<SMALL, FU>(ib, near);
-#endif
     }
-#ifdef TFHE_GUARD_CHAINS
     near = min(near, min(min(nq[0], nq[1]), min(nq[2], nq[3])));
-#endif
 }
 
 // Forward transforms + MAC of row pair (2RP, 2RP+1) against `bk` (the pair's
@@ -2762,6 +2754,29 @@ double blind_rotate_cost(size_t B, size_t cus) {
     return (double)(B / round) + wide(tail);
 }
 
+// Items [start, start + count) of a batch through one form: their ops / idx
+// entries / inputs / outputs / near-tie flags.
+static hipError_t launch_blind_rotate_range(const KParams &P, const DevTables &T, const uint8_t *ops,
+                                            const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                                            const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
+                                            size_t start, size_t count, hipStream_t s, char form, const LaunchOpts &O,
+                                            const char **used) {
+    const size_t in_words = (size_t)P.n + 1;
+    const size_t out_words = out_mode == BR_OUT_LV1 ? (size_t)P.N + 1 : out_mode == BR_OUT_TRLWE ? 2 * (size_t)P.N : in_words;
+    KParams Q = P;
+    if (Q.tie_flags) Q.tie_flags += start;
+    return launch_blind_rotate_form(Q, T, ops ? ops + start : nullptr, idx ? in_a : in_a + start * in_words,
+                                    idx ? in_b : (in_b ? in_b + start * in_words : nullptr),
+                                    idx ? idx + 2 * start : nullptr, testvec, bkd, out + start * out_words, out_mode,
+                                    count, s, form, O, used);
+}
+
+// L = 1 (the UINT4 parameters) runs full rounds of the octo form (8 items x
+// #CUs): one octo round of 2,048 items takes 11.45 ms against 2 x 6.1 ms for
+// two whole-form rounds (profiles/r03e_guard_chains_lut_octo.txt, LUT 4,096: 22.9 vs 24.4 ms).
+// At L = 3 the octo form is 4-5 % slower than the whole form.
+static bool octo_rounds_pay(const KParams &P) { return P.L == 1; }
+
 static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T, const uint8_t *ops,
                                             const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                             const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
@@ -2770,22 +2785,28 @@ static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T
         const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : O.br_form == 5 ? 'o' : 'w';
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
-    if (B <= BR_WIDE_MAX_ITEMS)
-        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'W', O, used);
-    const size_t round = BR_WAVES * device_cus(), tail = B % round;
-    if (tail == 0 || tail > BR_TAIL_WIDE_MAX || B < round)
-        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'w', O, used);
-    const size_t main = B - tail;
-    hipError_t e = launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, main, s, 'w', O, used);
+    size_t done = 0;
+    const size_t octo_round = (size_t)BO_GATES * device_cus();
+    if (octo_rounds_pay(P) && B >= octo_round) {
+        done = B / octo_round * octo_round;
+        hipError_t e = launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, 0, done, s,
+                                                 'o', O, used);
+        if (e != hipSuccess || done == B) return e;
+        used = nullptr;
+    }
+    const size_t rest = B - done;
+    if (rest <= BR_WIDE_MAX_ITEMS)
+        return launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, done, rest, s, 'W',
+                                         O, used);
+    const size_t round = BR_WAVES * device_cus(), tail = rest % round;
+    if (tail == 0 || tail > BR_TAIL_WIDE_MAX || rest < round)
+        return launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, done, rest, s, 'w',
+                                         O, used);
+    hipError_t e = launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, done,
+                                             rest - tail, s, 'w', O, used);
     if (e != hipSuccess) return e;
-    // the tail: items main..B-1 (their ops / idx entries / inputs / outputs / near-tie flags)
-    const size_t in_words = (size_t)P.n + 1;
-    const size_t out_words = out_mode == BR_OUT_LV1 ? (size_t)P.N + 1 : out_mode == BR_OUT_TRLWE ? 2 * (size_t)P.N : in_words;
-    KParams Q = P;
-    if (Q.tie_flags) Q.tie_flags += main;
-    return launch_blind_rotate_form(Q, T, ops ? ops + main : nullptr, idx ? in_a : in_a + main * in_words,
-                                    idx ? in_b : (in_b ? in_b + main * in_words : nullptr), idx ? idx + 2 * main : nullptr,
-                                    testvec, bkd, out + main * out_words, out_mode, tail, s, 'W', O, nullptr);
+    return launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B - tail, tail, s, 'W',
+                                     O, nullptr);
 }
 
 // The margin guard's recompute: the whole form in the
