@@ -290,10 +290,11 @@ def test_circuit_schedule_round_packing_host():
     assert (packed[1024:1064] == 2).all() and (packed[:1024] == 1).all()
     _check_schedule(c, packed)
     # a 64-CU device: rounds of 256 gates, 1,064 = 4 rounds + a 40-gate tail
-    # (one latency-form pass); moving the 40 would make level 2's 140 gates take
-    # three latency-form passes instead of two: a tie, so nothing moves
+    # (one latency-form pass, 0.43 round); level 2's 100 gates take two passes
+    # (0.86).  Moved, level 2's 140 gates run as one whole-form round (1.0, cheaper
+    # than three passes at 1.29; blind_rotate_plan): 5.0 < 5.29, so the 40 move
     p64, _ = c.schedule(64)
-    assert np.array_equal(p64, plain)
+    assert np.array_equal(p64, packed)
 
 
 def test_circuit_schedule_mixed_config4_host():

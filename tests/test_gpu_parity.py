@@ -309,26 +309,28 @@ def test_lut_config5_full_4096_uint4(oracle):
     assert np.array_equal(out[idx], want)
 
 
-@pytest.mark.parametrize("extra", [0, 300, 1500])
-def test_lut_uint4_octo_rounds_and_tails(oracle, extra):
-    """L = 1 dispatch (launch_blind_rotate_forms): full octo rounds (8 items x
-    #CUs) then the rest by the whole / latency policy (extra 300: latency-form
-    tail; 1,500: one whole-form round + a latency-form tail).  Bit-identical to
-    the forced whole form, and to the oracle at the range boundaries."""
+@pytest.mark.parametrize("extra,form", [(0, "octo"), (300, "whole"), (1500, "octo"), (-1848, "wide")])
+def test_lut_uint4_dispatch_plans(oracle, extra, form):
+    """L = 1 dispatch (blind_rotate_plan): 8 x #CUs items and 8 x #CUs + 1,500
+    run the octo form (1.9 whole-form rounds per octo round), 8 x #CUs + 300 the
+    whole form in one launch (3 rounds beat 2 octo rounds), 200 items the latency
+    form.  Bit-identical to the forced whole form, and to the oracle at the
+    round boundaries."""
     import torch
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     c, k = ctx_for(oracle, "uint4")
-    B = 8 * cus + extra
+    B = 8 * cus + extra * cus // 256
     tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (3 * x + 1) % 16)
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
     msgs = rng(B).integers(0, 16, B).astype(np.uint32)
     cts = sk.encrypt_lwe_message(msgs, 16, seed0=B)
     out = c.bootstrap_lut_batch(cts, tv)
-    assert c.last_kernels().startswith("k_blind_rotate_octo<1,")
+    prefix = {"octo": "k_blind_rotate_octo<1,", "whole": "k_blind_rotate<1,", "wide": "k_blind_rotate_wide<1,"}[form]
+    assert c.last_kernels().startswith(prefix), c.last_kernels()
     with c.options(br_form="whole"):
         assert np.array_equal(c.bootstrap_lut_batch(cts, tv), out)
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (3 * msgs + 1) % 16)
-    idx = sorted({0, 8 * cus - 1, min(8 * cus, B - 1), min(8 * cus + 1024, B - 1), B - 1})
+    idx = sorted({0, min(4 * cus, B - 1), min(8 * cus - 1, B - 1), min(8 * cus, B - 1), B - 1})
     want = oracle.gate_batch(k.p, np.full(len(idx), 255, np.uint8), cts[idx], cts[idx], k.ck, testvec=tv,
                              threads=len(idx))
     assert np.array_equal(out[idx], want)

@@ -298,10 +298,13 @@ int sync_check(tfhe_gpu_ctx *c) {
     HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     std::string what;
-    if (e & DEV_ERR_GATE_WAIT) what += " a gate wave's wait for a BK slot";
-    if (e & DEV_ERR_LOADER_WAIT) what += std::string(what.empty() ? "" : " and") + " a loader wave's wait for a free BK slot";
+    if (e & DEV_ERR_GATE_WAIT) what += "slot-counter protocol failure: a gate wave's wait for a BK slot timed out";
+    if (e & DEV_ERR_LOADER_WAIT)
+        what += std::string(what.empty() ? "slot-counter protocol failure:" : " and") +
+                " a loader wave's wait for a free BK slot timed out";
+    if (e & DEV_ERR_LDS_LAYOUT) what += std::string(what.empty() ? "" : "; ") + "LDS array not at address 0, nothing computed";
     return fail(c, TFHE_ERR_DEVICE,
-                "blind rotation: slot-counter protocol failure:" + what + " timed out (device error word 0x" +
+                "blind rotation: " + what + " (device error word 0x" +
                     [&] { char b[16]; std::snprintf(b, sizeof b, "%x", e); return std::string(b); }() +
                     "); the outputs of the work since the last synchronisation are invalid");
 }

@@ -42,6 +42,7 @@ struct KParams {
 enum DevErr : uint32_t {
     DEV_ERR_GATE_WAIT = 1u,    // a gate wave's wait for a published BK slot timed out
     DEV_ERR_LOADER_WAIT = 2u,  // a loader wave's wait for a retired BK slot timed out
+    DEV_ERR_LDS_LAYOUT = 4u,   // the blind rotation's LDS array is not at address 0 (gather_rot)
 };
 // Default bound of one slot-counter wait (sleep units).
 constexpr uint32_t BR_SPIN_CAP_DEFAULT = 1u << 22;
@@ -95,7 +96,7 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
 // launch_blind_rotate's modelled time for B items on `cus` CUs, in whole-form
 // rounds of 4 x cus items (the circuit scheduler's level packing)
 size_t device_cus();
-double blind_rotate_cost(size_t B, size_t cus);
+double blind_rotate_cost(size_t B, size_t cus, int L = 3);
 // dst[k] = (negate ? -1 : 1) * src[idx[k]] for k < count, n+1 words each
 // (TLWELv0.neg: gates.zig:132-135)
 hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint32_t *idx, uint32_t *dst,

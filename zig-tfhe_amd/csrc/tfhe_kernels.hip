@@ -551,6 +551,45 @@ DEV double digit_f64(uint32_t x, int level, int bgbit) {
     return (double)(int32_t)d;
 }
 
+// The whole and octo forms keep tmp words with the top bit of every
+// decomposition field flipped (x ^ digit_msbs): the signed bgbit-bit field of
+// x ^ (Bg/2 << s) is ((x >> s) & (Bg - 1)) - Bg/2, digit_f64's digit, in one
+// v_bfe_i32 instead of a shift, a mask and a subtract (flipping a field's top
+// bit adds Bg/2 modulo Bg; the signed read maps [Bg/2, Bg) to [-Bg/2, 0)).
+DEV uint32_t digit_msbs(int L, int bgbit) {
+    uint32_t m = 0;
+    for (int l = 0; l < L; l++) m |= 1u << (31 - l * bgbit);
+    return m;
+}
+DEV double digit_f64_flipped(uint32_t xf, int level, int bgbit) {
+    return (double)(int32_t)__builtin_amdgcn_sbfe(xf, 32 - (level + 1) * bgbit, bgbit);
+}
+
+// tmp word of the rotation gather, flipped: ((neg ? -v : v) - acc + offset) ^ msbs
+// with s = neg ? ~0 : 0 and off_s = offset - s, since (v ^ s) - s = (neg ? -v : v).
+DEV uint32_t tmp_word(uint32_t v, uint32_t s, uint32_t off_s, uint32_t acc, uint32_t msbs) {
+    return ((v ^ s) + (off_s - acc)) ^ msbs;
+}
+
+// Rotation gather (polyMulWithXK, trgsw.zig:442-466) from an accumulator copy in
+// LDS at a 4 KB-aligned byte address `base` (a at words [0, 1024), b at
+// [1024, 2048)): lane word m is coefficient t + 64m, at byte index
+// xb[m] = 4 ((t - a~) mod 2N) + 256 m; its word is at (xb & 0xFFC) | base (one
+// v_and_or) and its negacyclic sign is bit 12 of xb (gather_sign).
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32_t;
+DEV uint32_t lds_read_u32(uint32_t byte_addr) { return *(lds_cu32_t *)(size_t)byte_addr; }
+DEV void gather_rot(uint32_t base, int t, int at, uint32_t *xb, uint32_t *tA, uint32_t *tB) {
+    const uint32_t rbb = (uint32_t)((t - at) & 2047) << 2;
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        xb[m] = rbb + 256u * m;
+        const uint32_t a = (xb[m] & 0xFFCu) | base;
+        tA[m] = lds_read_u32(a);
+        tB[m] = lds_read_u32(a + 4096u);
+    }
+}
+DEV uint32_t gather_sign(uint32_t xb) { return (uint32_t)__builtin_amdgcn_sbfe(xb, 12, 1); }
+
 // X^k rotation read (polyMulWithXK, trgsw.zig:442-466) of coefficient k from
 // the accumulator polynomial `p` (N=1024) held in LDS, k in [0, 2N].
 DEV uint32_t rot_read(const uint32_t *p, int k, int at) {
@@ -755,6 +794,13 @@ constexpr int BR_LDS_AT = 1024 * 2;                   // per wave
 constexpr int BR_LDS_SYNC = 64;                      // slot counters of the flag-synchronised variant
 constexpr int BR_LDS_TOTAL =
     BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST + BR_WAVES * (BR_LDS_ACC + BR_LDS_X + BR_LDS_AT) + BR_LDS_SYNC;
+constexpr int BR_LDS_ACC_AT = BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;  // accumulator copies: 4 KB-aligned (gather_rot)
+static_assert(BR_LDS_ACC_AT % 4096 == 0 && BR_LDS_ACC % 4096 == 0, "gather_rot needs 4 KB-aligned copies");
+
+// The kernel's one __shared__ array is the whole static LDS allocation and sits
+// at LDS address 0, so the offsets above are absolute; hipcc folds this check
+// (a constant address) away, and a layout that broke it fails loudly.
+DEV bool lds_layout_bad(const void *smem) { return ((uint32_t)(size_t)(const lds_void_t *)smem & 4095u) != 0; }
 
 // Flag-synchronised loader variant (FLAGS; TFHE_OPT_BR_SYNC = 1): instead of one
 // workgroup barrier per row pair, monotonic LDS counters per BK slot.  A
@@ -849,7 +895,8 @@ DEV void load_digits_lds(C2 *d, const uint32_t *s_tmp, int row, int L, int bgbit
     }
 }
 
-// Digits of rows (row, row+1) with one read of the 8 twist factors for both.
+// Digits of rows (row, row+1) with one read of the 8 twist factors for both
+// (flipped tmp words, digit_f64_flipped).
 template <bool FU = false>
 DEV void load_digits_pair_lds(C2 (*d)[8], const uint32_t *s_tmp, int row, int L, int bgbit, const C2 *twist_t,
                               int t) {
@@ -867,8 +914,8 @@ DEV void load_digits_pair_lds(C2 (*d)[8], const uint32_t *s_tmp, int row, int L,
         const C2 w = twist_t[64 * m];
 #pragma unroll
         for (int f = 0; f < 2; f++)
-            d[f][q] = twist_in<FU>(digit_f64(src[f][64 * m], level[f], bgbit),
-                                   digit_f64(src[f][64 * (m + 8)], level[f], bgbit), w);
+            d[f][q] = twist_in<FU>(digit_f64_flipped(src[f][64 * m], level[f], bgbit),
+                                   digit_f64_flipped(src[f][64 * (m + 8)], level[f], bgbit), w);
     }
 }
 
@@ -891,7 +938,7 @@ DEV void load_digits_pair0_regs(C2 (*d)[8], const uint32_t *tA, const uint32_t *
             const bool from_a = f < L;
             const uint32_t *src = from_a ? tA : tB;
             const int level = from_a ? f : f - L;
-            d[f][q] = twist_in<FU>(digit_f64(src[m], level, bgbit), digit_f64(src[m + 8], level, bgbit), w);
+            d[f][q] = twist_in<FU>(digit_f64_flipped(src[m], level, bgbit), digit_f64_flipped(src[m + 8], level, bgbit), w);
         }
     }
 }
@@ -1000,6 +1047,10 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     double2 *s_bk = reinterpret_cast<double2 *>(smem);
     // FLAGS: pub[2], done[2] (zeroed by the gate waves before the prologue barrier)
     uint32_t *s_sync = reinterpret_cast<uint32_t *>(smem + BR_LDS_TOTAL - BR_LDS_SYNC);
+    if (lds_layout_bad(smem)) {
+        if (tid == 0) __hip_atomic_fetch_or(P.err, (uint32_t)DEV_ERR_LDS_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (!FU && P.fallback) {  // reference-tree recompute: only workgroups with a flagged item
         const size_t g0 = (size_t)blockIdx.x * BR_WAVES;
         uint32_t any = 0;
@@ -1120,6 +1171,8 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     uint32_t near = NEAR_NONE;  // FU: margin guard (torus_from_f64_guarded)
     uint32_t fail = 0;  // FLAGS: a slot wait gave up (report_wait_failure)
     const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
+    const uint32_t msbs = digit_msbs(L, P.bgbit);
+    const uint32_t acc_base = (uint32_t)(size_t)(lds_void_t *)s_acc;  // 4 KB-aligned (BR_LDS_ACC_AT)
 
     for (int i = 0; i < n; i++) {
         pp.mark(0);
@@ -1133,13 +1186,8 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
 #ifndef TFHE_KO_TMP
         // all 32 gathers first (one wait), then the arithmetic: interleaved,
         // hipcc waits for every gather before issuing the next
-        const int rb = (t - at) & 2047;
-#pragma unroll
-        for (int m = 0; m < 16; m++) {
-            const int j = (rb + 64 * m) & 1023;
-            tA[m] = s_acc[j];
-            tB[m] = s_acc[1024 + j];
-        }
+        uint32_t xb[16];
+        gather_rot(acc_base, t, at, xb, tA, tB);
         // pair 0's twist factors ride with the gather (one wait for both);
         // read after the tmp stores they queued behind them (6.64 -> 6.61 ms,
         // profiles/r02_ab_twist_preload.txt)
@@ -1150,9 +1198,9 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 0; m < 16; m++) {
-            const bool neg = ((rb + 64 * m) & 1024) != 0;  // X^a~ wraps past N: negacyclic sign
-            tA[m] = (neg ? 0u - tA[m] : tA[m]) - accA[m] + P.offset;
-            tB[m] = (neg ? 0u - tB[m] : tB[m]) - accB[m] + P.offset;
+            const uint32_t sg = gather_sign(xb[m]), off_s = P.offset - sg;  // X^a~ wraps past N: negacyclic sign
+            tA[m] = tmp_word(tA[m], sg, off_s, accA[m], msbs);
+            tB[m] = tmp_word(tB[m], sg, off_s, accB[m], msbs);
         }
 #else
 #pragma unroll
@@ -1239,6 +1287,8 @@ constexpr int BO_LDS_BUF = 2048 * 4;  // per gate: accumulator / exchange buffer
 constexpr int BO_LDS_AT = 1024 * 2;   // per gate
 constexpr int BO_LDS_TOTAL = BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST + BO_GATES * (BO_LDS_BUF + BO_LDS_AT);
 static_assert(BO_LDS_TOTAL <= 160 * 1024, "octo form LDS");
+constexpr int BO_LDS_BUF_AT = BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;  // gate buffers: 4 KB-aligned (gather_rot)
+static_assert(BO_LDS_BUF_AT % 4096 == 0 && BO_LDS_BUF % 4096 == 0, "gather_rot needs 4 KB-aligned buffers");
 
 // LDS-DMA of one BK row pair (32 KB) into a slot by 512 threads: 4 x 16 B each,
 // in the scalar-base form (SGPR pair address + the thread's 32-bit byte
@@ -1270,7 +1320,7 @@ DEV void load_digits_row_regs(C2 *d, const uint32_t *tA, const uint32_t *tB, int
     for (int q = 0; q < 8; q++) {
         const int m = br3(q);
         const uint32_t x0 = from_a ? tA[m] : tB[m], x1 = from_a ? tA[m + 8] : tB[m + 8];
-        d[q] = twist_in<FU>(digit_f64(x0, level, bgbit), digit_f64(x1, level, bgbit), twist_t[64 * m]);
+        d[q] = twist_in<FU>(digit_f64_flipped(x0, level, bgbit), digit_f64_flipped(x1, level, bgbit), twist_t[64 * m]);
     }
 }
 
@@ -1358,6 +1408,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_octo(
     const int op = ops ? (int)ops[g] : 255;
     const uint32_t pairs = (uint32_t)n * L;
 
+    if (lds_layout_bad(smem)) {
+        if (tid == 0) __hip_atomic_fetch_or(P.err, (uint32_t)DEV_ERR_LDS_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     issue_bk_pair_async512(bkd, s_bk, tid);  // pair 0 into slot 0, lands under the prologue
     for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
     for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
@@ -1383,25 +1437,22 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_octo(
     const C2 *twist_t = s_twist + t;
     int at_next = s_at[0];
     uint32_t near = NEAR_NONE;
+    const uint32_t msbs = digit_msbs(L, P.bgbit);
+    const uint32_t buf_base = (uint32_t)(size_t)(lds_void_t *)s_buf;  // 4 KB-aligned (BO_LDS_BUF_AT)
 
     for (int i = 0; i < n; i++) {
         const int at = __builtin_amdgcn_readfirstlane(at_next);
         at_next = s_at[i + 1 < n ? i + 1 : i];
         // tmp = X^{a~} acc - acc + offset, kept in registers for every row's digits
         uint32_t tA[16], tB[16];
-        const int rb = (t - at) & 2047;
-#pragma unroll
-        for (int m = 0; m < 16; m++) {
-            const int j = (rb + 64 * m) & 1023;
-            tA[m] = s_buf[j];
-            tB[m] = s_buf[1024 + j];
-        }
+        uint32_t xb[16];
+        gather_rot(buf_base, t, at, xb, tA, tB);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 0; m < 16; m++) {
-            const bool neg = ((rb + 64 * m) & 1024) != 0;  // X^a~ wraps past N: negacyclic sign
-            tA[m] = (neg ? 0u - tA[m] : tA[m]) - accA[m] + P.offset;
-            tB[m] = (neg ? 0u - tB[m] : tB[m]) - accB[m] + P.offset;
+            const uint32_t sg = gather_sign(xb[m]), off_s = P.offset - sg;  // X^a~ wraps past N: negacyclic sign
+            tA[m] = tmp_word(tA[m], sg, off_s, accA[m], msbs);
+            tB[m] = tmp_word(tB[m], sg, off_s, accB[m], msbs);
         }
         wave_sync();  // the gather's reads precede the exchanges' writes into the buffer
         C2 fa[8], fb[8];
@@ -2721,14 +2772,26 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     return hipGetLastError();
 }
 
-// Kernel form per batch.  LaunchOpts::br_form (TFHE_OPT_BR_FORM) forces one
-// form for the whole batch (A/B runs and tests).  Otherwise: the latency form up to
-// BR_WIDE_MAX_ITEMS; above it the whole form, except that a ragged last round
-// of at most BR_TAIL_WIDE_MAX items (the whole form runs 4 items x #CUs per
-// round) goes to the latency form, which takes ~4.2 ms for up to 256 items and
-// ~8.1 ms for up to 512 instead of a full ~9.5 ms round (a circuit level of
-// 10,256 gates: 99 vs 106 ms).
+// Modelled blind-rotation time on a device with `cus` CUs, in whole-form
+// rounds (BR_WAVES x cus items), of the launch plans launch_blind_rotate picks
+// from; the cheapest wins (ties: the earlier plan).  LaunchOpts::br_form
+// (TFHE_OPT_BR_FORM) instead forces one form for the whole batch (A/B runs, tests).
+//  - latency form for the whole batch (at most BR_WIDE_MAX_ITEMS): per item per
+//    CU 0.43 of a round at L = 3 (4.1 ms for up to 256 items, 8.1 ms for 512, a
+//    round 9.6 ms), BR_WIDE_COST_L1 at L = 1 (a round 6.05 ms);
+//  - whole form for the whole batch, ceil(B / round) rounds;
+//  - whole form for the full rounds and the latency form for a ragged tail of at
+//    most BR_TAIL_WIDE_MAX items (a circuit level of 10,256 gates: 99 vs 106 ms);
+//  - L = 1: the octo form for the whole batch, BO_ROUND_COST_L1 per octo round
+//    (8 x cus items).  One octo round costs 1.9 whole-form rounds (2,048 items:
+//    11.50 vs 12.09 ms, 4,096: 22.6 vs 23.9, 8,192: 44.9 vs 47.3).  At L = 3 the
+//    octo form is 4-5 % slower than the whole form.  Octo rounds
+//    followed by a tail launch measured 2 ms worse than modelled (2,348 items:
+//    19.5 ms against 17.6 for three whole-form rounds), so that split is no plan
+//    (profiles/r03g_octo_dispatch.txt).
 constexpr size_t BR_TAIL_WIDE_MAX = BR_WIDE_MAX_ITEMS;
+constexpr double BO_ROUND_COST_L1 = 1.9;
+constexpr double BR_WIDE_COST_L1 = 0.66;
 
 size_t device_cus() {
     static int cus = [] {
@@ -2740,18 +2803,35 @@ size_t device_cus() {
     return (size_t)cus;
 }
 
-// Modelled time of launch_blind_rotate(B) on a device with `cus` CUs, in
-// whole-form rounds (BR_WAVES x cus items), following its dispatch: the
-// latency form takes ~0.43 of a round per item per CU (4.1 ms
-// for up to 256 items, 8.1 ms for 512, a round 9.6 ms).
-double blind_rotate_cost(size_t B, size_t cus) {
-    if (B == 0) return 0.0;
-    const size_t round = BR_WAVES * cus;
-    auto wide = [&](size_t b) { return 0.43 * (double)((b + cus - 1) / cus); };
-    if (B <= BR_WIDE_MAX_ITEMS) return wide(B);
-    const size_t tail = B % round;
-    if (tail == 0 || tail > BR_TAIL_WIDE_MAX || B < round) return (double)((B + round - 1) / round);
-    return (double)(B / round) + wide(tail);
+enum BrPlan { PLAN_NONE, PLAN_WIDE, PLAN_WHOLE, PLAN_WHOLE_TAIL, PLAN_OCTO };
+
+static BrPlan blind_rotate_plan(size_t B, size_t cus, int L, double *cost_out) {
+    if (B == 0) {
+        if (cost_out) *cost_out = 0.0;
+        return PLAN_NONE;
+    }
+    const size_t round = BR_WAVES * cus, tail = B % round;
+    const double kw = L == 1 ? BR_WIDE_COST_L1 : 0.43;
+    auto wide = [&](size_t b) { return kw * (double)((b + cus - 1) / cus); };
+    BrPlan best = PLAN_WHOLE;
+    double c = (double)((B + round - 1) / round);
+    auto consider = [&](BrPlan p, double v) {
+        if (v < c) best = p, c = v;
+    };
+    if (B <= BR_WIDE_MAX_ITEMS && wide(B) <= c) best = PLAN_WIDE, c = wide(B);
+    if (tail != 0 && tail <= BR_TAIL_WIDE_MAX && B >= round) consider(PLAN_WHOLE_TAIL, (double)(B / round) + wide(tail));
+    if (L == 1) {
+        const size_t octo_round = (size_t)BO_GATES * cus;
+        consider(PLAN_OCTO, BO_ROUND_COST_L1 * (double)((B + octo_round - 1) / octo_round));
+    }
+    if (cost_out) *cost_out = c;
+    return best;
+}
+
+double blind_rotate_cost(size_t B, size_t cus, int L) {
+    double c = 0.0;
+    blind_rotate_plan(B, cus, L, &c);
+    return c;
 }
 
 // Items [start, start + count) of a batch through one form: their ops / idx
@@ -2771,12 +2851,6 @@ static hipError_t launch_blind_rotate_range(const KParams &P, const DevTables &T
                                     count, s, form, O, used);
 }
 
-// L = 1 (the UINT4 parameters) runs full rounds of the octo form (8 items x
-// #CUs): one octo round of 2,048 items takes 11.45 ms against 2 x 6.1 ms for
-// two whole-form rounds (profiles/r03e_guard_chains_lut_octo.txt, LUT 4,096: 22.9 vs 24.4 ms).
-// At L = 3 the octo form is 4-5 % slower than the whole form.
-static bool octo_rounds_pay(const KParams &P) { return P.L == 1; }
-
 static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T, const uint8_t *ops,
                                             const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                             const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
@@ -2785,28 +2859,23 @@ static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T
         const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : O.br_form == 5 ? 'o' : 'w';
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
-    size_t done = 0;
-    const size_t octo_round = (size_t)BO_GATES * device_cus();
-    if (octo_rounds_pay(P) && B >= octo_round) {
-        done = B / octo_round * octo_round;
-        hipError_t e = launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, 0, done, s,
-                                                 'o', O, used);
-        if (e != hipSuccess || done == B) return e;
-        used = nullptr;
+    const size_t round = BR_WAVES * device_cus(), tail = B % round;
+    switch (blind_rotate_plan(B, device_cus(), P.L, nullptr)) {
+    case PLAN_NONE: return hipSuccess;
+    case PLAN_WIDE:
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'W', O, used);
+    case PLAN_OCTO:
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'o', O, used);
+    case PLAN_WHOLE_TAIL: {
+        hipError_t e = launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, 0, B - tail,
+                                                 s, 'w', O, used);
+        if (e != hipSuccess) return e;
+        return launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B - tail, tail, s,
+                                         'W', O, nullptr);
     }
-    const size_t rest = B - done;
-    if (rest <= BR_WIDE_MAX_ITEMS)
-        return launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, done, rest, s, 'W',
-                                         O, used);
-    const size_t round = BR_WAVES * device_cus(), tail = rest % round;
-    if (tail == 0 || tail > BR_TAIL_WIDE_MAX || rest < round)
-        return launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, done, rest, s, 'w',
-                                         O, used);
-    hipError_t e = launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, done,
-                                             rest - tail, s, 'w', O, used);
-    if (e != hipSuccess) return e;
-    return launch_blind_rotate_range(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B - tail, tail, s, 'W',
-                                     O, nullptr);
+    default:
+        return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, 'w', O, used);
+    }
 }
 
 // The margin guard's recompute: the whole form in the

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "8f9a288a25ac410a"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "e2b3a4ec3adbd578"; }
