@@ -121,8 +121,8 @@ int tfhe_gpu_num_devices(const tfhe_gpu_ctx *ctx);
  * number of devices.  Shows where a sharded batch or circuit ran. */
 int tfhe_gpu_device_bootstraps(const tfhe_gpu_ctx *ctx, uint64_t *counts, int max_devices);
 /* Items whose blind rotation the fused arithmetic's margin guard sent to the
- * reference-tree recompute since the context was created (a value rounded
- * within 1/8 of a tie), as of the last synchronisation. */
+ * reference-tree recompute since the context was created (a value 1/4 or
+ * more off its integer), as of the last synchronisation. */
 int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
 
 /* ---- Options (kernel forms and table sources; default = the measured-
@@ -159,11 +159,11 @@ enum {
 };
 /* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
  * runs fused multiply-adds in the reference's operation order, with a margin
- * guard: every value it rounds must lie within 3/8 of an integer (the fused
- * and the reference's values differ by <= 2^-6); an item that
- * rounded anything closer to a tie is recomputed in the reference's expression
- * trees in the same stream (tfhe_gpu_near_tie_items counts them), so both
- * round to the same integers.  UINT4: the reference's trees.
+ * guard: every value it rounds must lie within 1/4 of an integer (the fused
+ * and the reference's values differ by less than 1/8); an item
+ * that rounded anything further off is recomputed in the reference's
+ * expression trees in the same stream (tfhe_gpu_near_tie_items counts them),
+ * so both round to the same integers.  UINT4: the reference's trees.
  * TFHE_ARITH_REFERENCE: the reference's expression trees everywhere. */
 enum { TFHE_ARITH_AUTO = 0, TFHE_ARITH_REFERENCE = 1 };
 /* The two libm candidates a Zig build of the reference can bind @cos/@sin to

@@ -241,7 +241,7 @@ double oracle_trig_sin(double x, int source) { return source == 1 ? fd_sin(x) : 
  * operation order are unchanged.  Test infrastructure, like the rest. */
 /* 2 = "guarded": fused, plus the kernels' margin guard (torus_from_f64_guarded,
  * tfhe_kernels.hip): a blind rotation that rounds a value with
- * rint(4v + 2) = 0 mod 4 (|v - rint(v)| >= 3/8, via the same f64 add as the
+ * rint(2v + 1) even (|v - rint(v)| >= 1/4, via the same f64 add as the
  * kernel) is redone in the reference's trees — the MI355X default.  FUSED is
  * the arithmetic in force on this thread (a guarded recompute forces 0). */
 static int g_fused = 0, g_guard = 0;
@@ -436,11 +436,11 @@ void oracle_fft(uint32_t N, const double *in, uint32_t *out) {
         int64_t rr = (int64_t)(FUSED ? nearbyint(tmp_re) : round(tmp_re));
         int64_t ri = (int64_t)(FUSED ? nearbyint(tmp_im) : round(tmp_im));
         if (FUSED && g_guard) {
-            double s_re = tmp_re + 1688849860263936.5, s_im = tmp_im + 1688849860263936.5;  /* 1.5*2^50 + 0.5 */
+            double s_re = tmp_re + 3377699720527872.5, s_im = tmp_im + 3377699720527872.5;  /* 1.5*2^51 + 0.5 */
             uint64_t b_re, b_im;
             memcpy(&b_re, &s_re, 8);
             memcpy(&b_im, &s_im, 8);
-            if ((b_re & 3u) == 0 || (b_im & 3u) == 0) tl_near = 1;
+            if ((b_re & 1u) == 0 || (b_im & 1u) == 0) tl_near = 1;  /* rint(2v + 1) even: |v - rint(v)| >= 1/4 */
         }
         double e_re = fabs(tmp_re - round(tmp_re)), e_im = fabs(tmp_im - round(tmp_im));
         if (e_re > tl_round_err) tl_round_err = e_re;

@@ -554,7 +554,7 @@ def test_margin_guard_recomputes_near_ties(oracle, form):
     """under a crafted key (conftest.crafted_near_tie_case) the
     unguarded fused arithmetic parts from the reference (the oracle's fused mode
     differs from its reference mode).  Every fused form returns the REFERENCE's
-    words: the items that rounded a value within 1/8 of a tie were flagged by
+    words: the items that rounded a value 1/4 or more off its integer were flagged by
     the margin guard and redone by the reference-tree recompute, which
     tfhe_gpu_near_tie_items counts.  (Honest batches never trigger it:
     test_margin_guard_quiet_on_honest_batches.)"""
@@ -588,7 +588,7 @@ def test_margin_guard_recomputes_near_ties(oracle, form):
 
 def test_margin_guard_quiet_on_honest_batches(oracle):
     """The seeded key and a 1,024-gate NAND batch of fresh encryptions (the
-    headline shape): no value comes within 3/8 of a tie (honest rotations stay
+    headline shape): no value comes 1/4 off its integer (honest rotations stay
     within ~0.11 of an integer), nothing is recomputed."""
     c, k = ctx_for(oracle, "128")
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)

@@ -310,7 +310,7 @@ def test_aligned_adversarial_digits_part_the_trees(oracle):
     misses the exact integer at ~0.1 % of outputs) and the reference's and the
     fused trees round some coefficients differently.  Their pre-rounding values
     stay within 1/8 of each other (measured max 0.094 over 3.3 M such outputs,
-    DESIGN.md §6.1), so the kernels' margin guard (|v - rint(v)| >= 3/8 ->
+    DESIGN.md §6.1), so the kernels' margin guard (|v - rint(v)| >= 1/4 ->
     recompute in the reference's trees) flags every coefficient where they part."""
     from oracle import params
     p = params("128")
@@ -335,11 +335,11 @@ def test_aligned_adversarial_digits_part_the_trees(oracle):
         delta = max(delta, float(np.abs(v0 - v1).max()))
         differ = w0 != w1
         part += int(differ.sum())
-        # the kernel's guard: v + (1.5*2^50 + 1/2) by one f64 add, mantissa bits 1:0 == 0
-        near = ((v1 + 1688849860263936.5).view(np.uint64) & np.uint64(3)) == 0
+        # the kernel's guard: v + (1.5*2^51 + 1/2) by one f64 add, mantissa bit 0 == 0
+        near = ((v1 + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0
         assert not (differ & ~near).any()  # every parting coefficient is flagged
     assert mag > 2 ** 47.5
-    assert delta < 0.125
+    assert delta < 0.125  # half the guard's 1/4 margin
     assert part > 0
 
 

@@ -503,21 +503,23 @@ DEV uint32_t torus_from_f64_small(double v) {
 }
 
 // Fused kernels (FU, the exact-integer regime of DESIGN.md §6.1), with the
-// margin guard.  The fused value v and the reference's value differ by far
-// less than 1/8 (measured <= 2^-6), so wherever v is more than
-// 1/8 from a tie both round to the same integer.  One add rounds v + 0.5 to a
-// multiple of 1/4: s = v + (1.5*2^50 + 0.5) (|v| < 2^49), whose mantissa is
-// 2^51 + Q with Q = rint(4v + 2).  Q >> 2 (mantissa bits 33..2, one
-// v_alignbit) is rint(v) and Q mod 4 = 0 exactly when |v - rint(v)| >= 3/8:
-// `near` keeps the minimum of (Q mod 4) over the launch, and a 0 sends the
-// item to the reference-tree recompute (near_tie_flag, k_blind_rotate FALLBACK).
+// margin guard.  The fused value v and the reference's value differ by less
+// than 1/4 (measured max 0.094 at the largest magnitude a keygen'd key admits,
+// DESIGN.md §6.1), so wherever v is within 1/4 of an integer both round to
+// that integer.  One add rounds v + 0.5 to a multiple of 1/2:
+// s = v + (1.5*2^51 + 0.5) (|v| < 2^49), whose mantissa is 2^51 + Q with
+// Q = rint(2v + 1).  Q odd <=> |v - rint(v)| < 1/4, and then Q >> 1 (mantissa
+// bits 32..1, one v_alignbit) is rint(v).  `near` ANDs the low words over the
+// launch (one v_bitop3 per two values); bit 0 clear sends the item to the
+// reference-tree recompute (near_tie_flag, k_blind_rotate FALLBACK), which
+// replaces every word of the item.
 DEV uint32_t torus_from_f64_guarded(double v, uint32_t &near) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v + 1688849860263936.5);
+    const uint64_t b = (uint64_t)__double_as_longlong(v + 3377699720527872.5);
     const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
-#ifndef TFHE_GUARD_NOMIN  // A/B timing builds only: the conversion without the flag
-    near = min(near, lo & 3u);
+#ifndef TFHE_GUARD_NOFLAG  // A/B timing builds only: the conversion without the flag
+    near &= lo;
 #endif
-    return __builtin_amdgcn_alignbit(hi, lo, 2);
+    return __builtin_amdgcn_alignbit(hi, lo, 1);
 }
 
 // Unguarded fused conversion (TFHE_FU_UNGUARDED A/B builds only): v + 1.5*2^52
@@ -535,12 +537,12 @@ DEV uint32_t to_torus(double v, uint32_t &near) {
 #endif
     return SMALL ? torus_from_f64_small(v) : torus_from_f64(v);
 }
-// Initial value of a `near` accumulator: no near tie seen.
-constexpr uint32_t NEAR_NONE = 3u;
+// Initial value of a `near` accumulator: no value off its integer by 1/4 or more.
+constexpr uint32_t NEAR_NONE = ~0u;
 // End of a fused item: if any lane of this wave rounded near a tie, flag item g
 // (one byte, a vector store; the flag is rare, the ballot is one SALU compare).
 DEV void near_tie_flag(const KParams &P, uint32_t near, size_t g, bool valid) {
-    if (__builtin_amdgcn_ballot_w64(near == 0u) != 0 && valid && P.tie_flags && (threadIdx.x & 63) == 0)
+    if (__builtin_amdgcn_ballot_w64((near & 1u) == 0u) != 0 && valid && P.tie_flags && (threadIdx.x & 63) == 0)
         P.tie_flags[g] = 1;
 }
 
@@ -580,10 +582,16 @@ typedef __attribute__((address_space(3))) const uint32_t lds_cu32_t;
 DEV uint32_t lds_read_u32(uint32_t byte_addr) { return *(lds_cu32_t *)(size_t)byte_addr; }
 DEV void gather_rot(uint32_t base, int t, int at, uint32_t *xb, uint32_t *tA, uint32_t *tB) {
     const uint32_t rbb = (uint32_t)((t - at) & 2047) << 2;
+    // hipcc splits (x & 0xFFC) | base into v_and + v_or; v_and_or_b32 with the
+    // mask in a VGPR (VOP3 takes no literal here, and base is the one SGPR)
+    const uint32_t mask = __builtin_amdgcn_readfirstlane(0xFFCu);
+    uint32_t vmask;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(vmask) : "s"(mask));
 #pragma unroll
     for (int m = 0; m < 16; m++) {
         xb[m] = rbb + 256u * m;
-        const uint32_t a = (xb[m] & 0xFFCu) | base;
+        uint32_t a;
+        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(xb[m]), "v"(vmask), "s"(base));
         tA[m] = lds_read_u32(a);
         tB[m] = lds_read_u32(a + 4096u);
     }
@@ -712,9 +720,10 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
 #ifndef TFHE_KO_INV
     fft512_x2<true, ONEBUF, FU>(e, xb, T, t);
 #endif
-    // four independent near-tie accumulators, joined at the end: one min chain
-    // would serialise 32 dependent v_min per call (A/B, profiles/r03e_guard_chains_lut_octo.txt:
-    // guard cost 0.8 % with four chains, 2.2 % with one)
+    // four independent near-tie accumulators, joined at the end: one chain
+    // would serialise its 32 updates per call (A/B with the round-3 min form,
+    // profiles/r03e_guard_chains_lut_octo.txt: guard cost 0.8 % with four chains,
+    // 2.2 % with one)
     uint32_t nq[4] = {NEAR_NONE, NEAR_NONE, NEAR_NONE, NEAR_NONE};
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -727,7 +736,7 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
         accB[q] += to_torus<SMALL, FU>(rb, nq[2]);
         accB[q + 8] += to_torus<SMALL, FU>(ib, nq[3]);
     }
-    near = min(near, min(min(nq[0], nq[1]), min(nq[2], nq[3])));
+    near &= nq[0] & nq[1] & nq[2] & nq[3];
 }
 
 // Forward transforms + MAC of row pair (2RP, 2RP+1) against `bk` (the pair's

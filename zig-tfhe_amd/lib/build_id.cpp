@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "e2b3a4ec3adbd578"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "ff7ea4a196060eeb"; }
