@@ -564,8 +564,9 @@ def main():
             "roofline_hbm_accounting": hbm,
             "key_switch": {"kernel": kernels.split(" + ")[-1], "avg_ms": round(ks_avg_s * 1e3, 3)},
             "margin_guard": {"recomputed_items": recomputed, "items": B * args.steps,
-                             "note": "fused arithmetic; items rounding within 1/8 of a tie are redone in the "
-                                     "reference's expression trees inside the timed launches (DESIGN.md §6.1)"},
+                             "note": "fused arithmetic; items that round a value 1/4 or more off its integer are "
+                                     "redone in the reference's expression trees inside the timed launches "
+                                     "(DESIGN.md §6.1)"},
             "kernel_build_id": kernel_build_id(),
             "kernel_source_sha256": kernel_source_hash(),
             "decrypt_check": all_correct,
