@@ -77,5 +77,33 @@ int main() {
         CK(hipStreamSynchronize(s));
         std::printf("staged H2D in 4 chunks, 1 thread: %.3f ms\n", (now() - t0) * 1e3);
     }
+    // concurrent pageable H2D / D2H: T host threads, each its own stream and slice
+    {
+        std::vector<hipStream_t> ss(8);
+        for (auto &x : ss) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        std::vector<char> back(in_bytes);
+        for (int th : {1, 2, 4, 8}) {
+            double best_h = 1e9, best_d = 1e9;
+            for (int rep = 0; rep < 5; rep++) {
+                for (int dir = 0; dir < 2; dir++) {
+                    double t0 = now();
+                    std::vector<std::thread> v;
+                    for (int k = 0; k < th; k++)
+                        v.emplace_back([&, k] {
+                            const size_t a = in_bytes * k / th, b = in_bytes * (k + 1) / th;
+                            if (dir == 0)
+                                (void)hipMemcpyAsync(dev + a, src.data() + a, b - a, hipMemcpyHostToDevice, ss[k]);
+                            else
+                                (void)hipMemcpyAsync(back.data() + a, dev + a, b - a, hipMemcpyDeviceToHost, ss[k]);
+                            (void)hipStreamSynchronize(ss[k]);
+                        });
+                    for (auto &x : v) x.join();
+                    (dir == 0 ? best_h : best_d) = std::min(dir == 0 ? best_h : best_d, now() - t0);
+                }
+            }
+            std::printf("concurrent pageable %.1f MB, %d thread(s)/stream(s): H2D %.3f ms (%.1f GB/s), D2H %.3f ms (%.1f GB/s)\n",
+                        in_bytes / 1e6, th, best_h * 1e3, rate(in_bytes, best_h), best_d * 1e3, rate(in_bytes, best_d));
+        }
+    }
     return 0;
 }

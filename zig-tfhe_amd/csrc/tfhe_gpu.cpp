@@ -288,9 +288,16 @@ int h2d(tfhe_gpu_ctx *c, DevBuf &buf, const void *src, size_t bytes) {
 // words are not the reference's).  The word is copied into pinned host memory
 // on the stream, so the one synchronisation covers both; a reported error is
 // cleared, and the context stays usable.
-int sync_check(tfhe_gpu_ctx *c) {
+// Queue the copy of the device error word (and the recompute counter) into
+// pinned host memory on the context stream.
+static int queue_err_copy(tfhe_gpu_ctx *c) {
     HIPCHK(c, hipMemcpyAsync(c->h_err, c->d_err, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return TFHE_OK;
+}
+
+// After a synchronisation that covered queue_err_copy: fail the call if a
+// kernel set the error word (clearing it; the context stays usable).
+static int check_err_word(tfhe_gpu_ctx *c) {
     c->near_tie_items = c->h_err[1];
     const uint32_t e = *c->h_err;
     if (!e) return TFHE_OK;
@@ -309,6 +316,13 @@ int sync_check(tfhe_gpu_ctx *c) {
                     "); the outputs of the work since the last synchronisation are invalid");
 }
 
+int sync_check(tfhe_gpu_ctx *c) {
+    int rc = queue_err_copy(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return check_err_word(c);
+}
+
 // 64-bit fingerprints of this context's device BK and KSK (k_checksum), synchronous.
 int key_fingerprint(tfhe_gpu_ctx *c, uint64_t &bk, uint64_t &ksk) {
     auto *d = reinterpret_cast<unsigned long long *>(c->d_err + 2);
@@ -325,9 +339,20 @@ int key_fingerprint(tfhe_gpu_ctx *c, uint64_t &bk, uint64_t &ksk) {
     return TFHE_OK;
 }
 
+// The outputs and the error word in one synchronisation: the word's copy is
+// queued first, so it has landed when the outputs have (one round trip fewer
+// than copying it after them: DESIGN.md §2.1).
 int d2h_sync(tfhe_gpu_ctx *c, void *dst, const void *src, size_t bytes) {
+    int rc = queue_err_copy(c);
+    if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    return sync_check(c);
+    // a pageable destination makes the copy synchronous: the stream is idle by
+    // now and hipStreamQuery says so at once, where hipStreamSynchronize on an
+    // idle stream still took ~19 us (profiles/r03_host_path_trace.txt)
+    const hipError_t q = hipStreamQuery(c->stream);
+    if (q == hipErrorNotReady) HIPCHK(c, hipStreamSynchronize(c->stream));
+    else HIPCHK(c, q);
+    return check_err_word(c);
 }
 
 // TLWELv0.encryptF64 (tlwe.zig:34-49) with DefaultPrng(seed).
