@@ -81,15 +81,34 @@ def test_external_product_vs_oracle(oracle, pname):
     assert np.array_equal(c.external_product(x, bk_index=5), want)
 
 
-@pytest.mark.parametrize("form", ["lanes", "lanes-narrow", "sel"])
+@pytest.mark.parametrize("form", ["lanes", "lanes-narrow", "sel", "gemm"])
 @pytest.mark.parametrize("pname,B", [("128", 9), ("128", 130), ("80", 1), ("80", 65), ("uint4", 17), ("uint4", 300)])
 def test_key_switch_vs_oracle(oracle, pname, B, form):
-    """All key-switch forms (lane = item in wide / narrow blocks, lane = word) bit-exact, ragged B."""
+    """All key-switch forms (lane = item in wide / narrow blocks, lane = word,
+    one-hot GEMM on the matrix cores) bit-exact, ragged B."""
     c, k = ctx_for(oracle, pname)
     lv1 = u32rand(rng(5), B, 1025)
     want = np.array([oracle.identity_key_switch(k.p, v, k.ck.ksk) for v in lv1])
-    with c.options(ks_form=int(form == "sel"), ks_narrow=int(form.endswith("narrow"))):
+    with c.options(ks_form={"sel": 1, "gemm": 2}.get(form, 0), ks_narrow=int(form.endswith("narrow"))):
         assert np.array_equal(c.key_switch(lv1), want)
+        if form == "gemm":
+            assert c.last_kernels().startswith("k_key_switch_gemm<") == (pname != "uint4")
+
+
+@pytest.mark.parametrize("B", [1024, 1500])
+def test_key_switch_gemm_full_batches(oracle, B):
+    """The gemm form at the headline batch (5 K splits over 220 workgroups) and
+    a ragged one: bit-identical to the lane form, and to the oracle on samples
+    from the first and last item groups and the last output tile."""
+    c, k = ctx_for(oracle, "128")
+    lv1 = u32rand(rng(B), B, 1025)
+    lanes = c.key_switch(lv1)
+    with c.options(ks_form=2):
+        got = c.key_switch(lv1)
+        assert c.last_kernels().startswith("k_key_switch_gemm<9>")
+    assert np.array_equal(got, lanes)
+    for i in (0, 511, 512, B - 1):
+        assert np.array_equal(got[i], oracle.identity_key_switch(k.p, lv1[i], k.ck.ksk))
 
 
 # ---- blind rotation / bootstrap ---------------------------------------------

@@ -112,6 +112,9 @@ struct tfhe_gpu_ctx {
     DevBuf s_a, s_b, s_out, s_lv1, s_ops, s_tv, s_tmp;
     DevBuf s_wires, s_cidx, s_cops;  // circuit evaluator: wire table, gather indices, op codes
     DevBuf s_ties;                   // near-tie flags (KParams::tie_flags), one byte per item, zero between launches
+    DevBuf s_kspart;                 // gemm key switch: the K splits' partial sums
+    uint32_t *d_ksk_gemm = nullptr;  // gemm key switch: the MFMA-layout KSK (ks_gemm_bytes), built from d_ksk
+    bool ksk_gemm_ok = false;        // d_ksk_gemm matches d_ksk
     // device timing (tfhe_gpu_profile_begin/end): 3 events per bootstrap launch
     bool profiling = false;
     std::vector<hipEvent_t> events;
@@ -204,6 +207,7 @@ size_t ksk_dev_bytes(const tfhe_params &p) {
 // host KSK (reference layout) -> device KSK (padded rows), async on the ctx stream
 int upload_ksk(tfhe_gpu_ctx *c, const uint32_t *ksk) {
     const size_t w = c->P.n + 1, stride = c->K.ks_stride;
+    c->ksk_gemm_ok = false;
     HIPCHK(c, hipMemsetAsync(c->d_ksk, 0, c->ksk_bytes, c->stream));
     HIPCHK(c, hipMemcpy2DAsync(c->d_ksk, stride * 4, ksk, w * 4, w * 4, ksk_rows(c->P), hipMemcpyHostToDevice,
                                c->stream));
@@ -236,6 +240,27 @@ enum RunKind : int {
     RUN_TRLWE = 1,         // the accumulator: TRLWELv1 (trgsw.zig:290-333)
     RUN_NO_KEYSWITCH = 2,  // sampleExtractIndex2, n+1 words (vanilla.zig:58-69)
 };
+
+// The gemm key switch's buffers for a batch of B (TFHE_OPT_KS_FORM = 2): the
+// MFMA-layout KSK, rebuilt on the stream after a key change, and the partial
+// sums.  G stays empty for the other forms (launch_key_switch ignores it).
+int ks_gemm_args(tfhe_gpu_ctx *c, size_t B, KsGemm &G) {
+    G = KsGemm();
+    if (c->opts.ks_form != 2 || !ks_gemm_supported(c->K)) return TFHE_OK;
+    if (!c->d_ksk_gemm) {
+        hipError_t e = hipMalloc((void **)&c->d_ksk_gemm, ks_gemm_bytes(c->K));
+        if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, "hipMalloc(ksk gemm layout)");
+    }
+    if (!c->ksk_gemm_ok) {
+        HIPCHK(c, launch_ksk_to_gemm(c->K, c->d_ksk, c->d_ksk_gemm, c->stream));
+        c->ksk_gemm_ok = true;
+    }
+    int rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B));
+    if (rc) return rc;
+    G.kg = c->d_ksk_gemm;
+    G.part = (uint32_t *)c->s_kspart.p;
+    return TFHE_OK;
+}
 
 // Blind rotation (+ key switch for RUN_BOOTSTRAP) over device buffers, async.
 int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, const uint32_t *b,
@@ -271,7 +296,11 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
     c->bootstraps += B;
     if (ev[1]) HIPCHK(c, hipEventRecord(ev[1], c->stream));
     c->last_ks = "";
-    if (key_switch) HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream, c->opts, &c->last_ks));
+    if (key_switch) {
+        KsGemm G;
+        if ((rc = ks_gemm_args(c, B, G))) return rc;
+        HIPCHK(c, launch_key_switch(c->K, lv1, c->d_ksk, out, B, c->stream, c->opts, &c->last_ks, &G));
+    }
     if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], c->stream));
     return TFHE_OK;
 }
@@ -499,7 +528,7 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)c->d_err, (void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
                     c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p, c->s_ties.p,
-                    c->s_wires.p, c->s_cidx.p, c->s_cops.p})
+                    c->s_wires.p, c->s_cidx.p, c->s_cops.p, c->s_kspart.p, (void *)c->d_ksk_gemm})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->h_err) (void)hipHostFree(c->h_err);
@@ -577,6 +606,7 @@ int tfhe_gpu_import_key_device(tfhe_gpu_ctx *c, const void *bsk_dev, const void 
     HIPCHK(c, hipMemcpyAsync(c->d_bk, bsk_dev, c->bk_bytes, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_ksk, ksk_dev, c->ksk_bytes, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, launch_ksk_zero_k0(c->K, c->d_ksk, c->stream));
+    c->ksk_gemm_ok = false;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_key = true;
     c->key_from_keygen = false;
@@ -1485,8 +1515,10 @@ static int key_switch_batch_one(tfhe_gpu_ctx *c, const uint32_t *in_lv1, uint32_
     int rc = h2d(c, c->s_lv1, in_lv1, B * 1025 * 4);
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
     if (rc) return rc;
+    KsGemm G;
+    if ((rc = ks_gemm_args(c, B, G))) return rc;
     HIPCHK(c, launch_key_switch(c->K, (const uint32_t *)c->s_lv1.p, c->d_ksk, (uint32_t *)c->s_out.p, B, c->stream,
-                                c->opts, &c->last_ks));
+                                c->opts, &c->last_ks, &G));
     return d2h_sync(c, out_lv0, c->s_out.p, B * w * 4);
 }
 
@@ -1557,8 +1589,8 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     bool ok = false;
     switch (key) {
     case TFHE_OPT_BR_FORM: ok = v >= 0 && v <= 5; break;
+    case TFHE_OPT_KS_FORM: ok = v >= 0 && v <= 2; break;
     case TFHE_OPT_BR_LOADER:
-    case TFHE_OPT_KS_FORM:
     case TFHE_OPT_KS_NARROW:
     case TFHE_OPT_CIRCUIT_PACK:
     case TFHE_OPT_BR_SYNC: ok = v == 0 || v == 1; break;
@@ -1771,6 +1803,7 @@ int broadcast_key(tfhe_gpu_ctx *c) {
         tfhe_gpu_ctx *s = c->shards[d];
         HIPCHK(c, hipSetDevice(s->device));
         HIPCHK(c, hipStreamSynchronize(s->stream));
+        s->ksk_gemm_ok = false;
     }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));

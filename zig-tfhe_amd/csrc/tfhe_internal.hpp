@@ -77,7 +77,7 @@ struct LaunchOpts {
     int br_form = 0;     // 0 auto, 1 whole, 2 split, 3 latency (wide), 4 pair
     int br_loader = 1;   // whole form: 1 loader waves issue the BK DMAs, 0 the gate waves do
     int br_flags = 1;    // whole form with loader waves: 1 slot counters (default), 0 a barrier per row pair
-    int ks_form = 0;     // 0 lanes, 1 select / gather
+    int ks_form = 0;     // 0 lanes, 1 select / gather, 2 one-hot GEMM on the matrix cores (basebit 2)
     int ks_narrow = 0;   // basebit 2: 1 forces the 32-word x 4-wave blocks
     int ks_groups = 0;   // basebit >= 5: item groups per block (0 auto = 4; 1, 2, 4, 8)
     int ks_sel_items = 8;  // select/gather form: items per block (8, 16, 32)
@@ -101,9 +101,19 @@ double blind_rotate_cost(size_t B, size_t cus, int L = 3);
 // (TLWELv0.neg: gates.zig:132-135)
 hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint32_t *idx, uint32_t *dst,
                               size_t count, bool negate, hipStream_t s);
+// The gemm form's device buffers: the MFMA-layout KSK
+// (ks_gemm_bytes) and the K splits' partial sums (ks_gemm_part_bytes(B)).
+struct KsGemm {
+    const uint32_t *kg = nullptr;
+    uint32_t *part = nullptr;
+};
+size_t ks_gemm_bytes(const KParams &P);
+size_t ks_gemm_part_bytes(const KParams &P, size_t B);
+bool ks_gemm_supported(const KParams &P);
+hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, hipStream_t s);
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
                              uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),
-                             const char **used = nullptr);
+                             const char **used = nullptr, const KsGemm *G = nullptr);
 // zero the k = 0 rows (never read by the reference; the kernels subtract them unconditionally)
 hipError_t launch_ksk_zero_k0(const KParams &P, uint32_t *ksk, hipStream_t s);
 // same for a key-switch-shaped key over n_in input coefficients (proxy re-encryption key)

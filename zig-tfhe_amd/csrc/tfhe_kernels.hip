@@ -2197,6 +2197,161 @@ __global__ __launch_bounds__(256) void k_key_switch_gather(KParams P, const uint
     }
 }
 
+// ---------------------------------------------------------------------------
+// Identity key switch as a one-hot integer GEMM on the matrix cores ("gemm"
+// form, basebit 2).  out[m][w] = [w = n]·b_m − Σ_{i,j}
+// KSK[i][j][k_{m,i,j}][w] (keyswitch, key.zig / tlwe identityKeySwitch) is
+// C = A·K with A[m][(i,j,k)] = [k = digit j of item m's a_i] (0/1) and K the
+// KSK rows, mod 2^32.  K is split into its 4 byte planes, stored as int8
+// (byte − 128); per plane v_mfma_i32_32x32x32_i8 sums exactly in int32
+// (|Σ| ≤ N·t·128), and out = b − Σ_b (C_b << 8b) − N·t·128·0x01010101 (every
+// (i, j) selects exactly one row, k = 0 included: its zero row reads −128).
+// K-order per MFMA step: one level j, 8 coefficients i0..i0+7; lane half h
+// holds coefficients i0 + 4h + (e >> 2), candidate k = e & 3 in its 16 bytes
+// e (A and B pair by (h, e): tools/mfma_i8_probe.hip shows any common k
+// permutation is exact).  Workgroup: 8 waves (2 per SIMD), 512 items, one
+// 32-word output tile; wave v takes items 64v..64v+63 as two 32-row MFMA
+// tiles, 2 x 4 accumulators (128 VGPRs).  The B fragments of a coefficient
+// block (t levels x 4 planes x 1 KB) come by LDS-DMA into a double buffer,
+// one barrier per block; K splits over blockIdx.z write partial sums that
+// k_ks_gemm_reduce adds.
+constexpr int KG_WAVES = 8;
+constexpr int KG_ITEMS = 64 * KG_WAVES;  // items per workgroup
+typedef int kg_v4i __attribute__((ext_vector_type(4)));
+typedef int kg_v16i __attribute__((ext_vector_type(16)));
+
+// MFMA-layout KSK, built from the device KSK (k = 0 rows zeroed):
+// kg[j][ib][wt][b][lane][e] int8, lane = 32h + c: byte b of
+// KSK[i = 8ib + 4h + (e >> 2)][j][k = e & 3][w = 32wt + c] − 128 (w > n: 0 − 128).
+size_t ks_gemm_bytes(const KParams &P) {
+    const size_t w32 = (size_t)(P.n + 1 + 31) / 32;
+    return (size_t)P.iks_t * (1024 / 8) * w32 * 4 * 1024;
+}
+__global__ void k_ksk_to_gemm(KParams P, const uint32_t *__restrict__ ksk, uint32_t *__restrict__ kg, size_t words) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // one u32 = bytes e = 4q .. 4q+3
+    if (x >= words) return;
+    const int w32 = (P.n + 1 + 31) / 32;
+    const int q = (int)(x & 3), lane = (int)((x >> 2) & 63), b = (int)((x >> 8) & 3);
+    size_t r = x >> 10;
+    const int wt = (int)(r % w32);
+    r /= w32;
+    const int ib = (int)(r % (1024 / 8)), j = (int)(r / (1024 / 8));
+    const int h = lane >> 5, c = lane & 31;
+    const int i = 8 * ib + 4 * h + q, w = 32 * wt + c;
+    const size_t rs = (size_t)P.ks_stride;
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t word = w <= P.n ? ksk[((size_t)(4 * P.iks_t) * i + 4 * j + k) * rs + w] : 0u;
+        v |= (((word >> (8 * b)) & 255u) ^ 128u) << (8 * k);  // byte − 128 as int8
+    }
+    kg[x] = v;
+}
+
+template <int T>
+__global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P, const uint32_t *__restrict__ lv1,
+                                                                   const uint32_t *__restrict__ kg,
+                                                                   uint32_t *__restrict__ part, size_t B,
+                                                                   int ib_per_split) {
+    constexpr int STEP_BYTES = 4 * 1024;  // one level's 4 planes of one 32-word tile
+    constexpr int BUF_BYTES = T * STEP_BYTES;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int v = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w32 = (P.n + 1 + 31) / 32;
+    const int wt = blockIdx.x;
+    const int ib_lo = blockIdx.z * ib_per_split, ib_hi = min(1024 / 8, ib_lo + ib_per_split);
+    const size_t m_base = (size_t)blockIdx.y * KG_ITEMS + 64 * v;
+    const int h = lane >> 5, c = lane & 31;
+    // this lane's two items (rows c of the wave's two MFMA tiles), clamped
+    const uint32_t *a_row[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const size_t m = m_base + 32 * s + c;
+        a_row[s] = lv1 + (m < B ? m : B - 1) * 1025;
+    }
+    // DMA of coefficient block ib: T x 4 KB, 512 threads x 16 B x (T/2 rounded up) ... one
+    // 16-B piece per thread per 8 KB: level pairs
+    const uint32_t lds0 = (uint32_t)(size_t)(lds_void_t *)smem;
+    auto issue = [&](int ib, int which) {
+#pragma unroll
+        for (int j = 0; j < T; j++) {
+            if (tid < 256) {  // 4 KB per level: 256 threads x 16 B
+                const uint32_t *src = kg + ((((size_t)j * (1024 / 8) + ib) * w32 + wt) * 1024 + tid * 16) / 4;
+                const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + which * BUF_BYTES + j * STEP_BYTES +
+                                                                    (tid & ~63) * 16);
+                uint32_t keep;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                    : "=&s"(keep)
+                    : "v"(src), "s"(dst)
+                    : "memory");
+            }
+        }
+    };
+    kg_v16i acc[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; s++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[s][b] = kg_v16i{};
+    const uint32_t prec = 1u << (32 - (1 + 2 * T));
+    if (ib_lo < ib_hi) issue(ib_lo, 0);
+    for (int ib = ib_lo; ib < ib_hi; ib++) {
+        const int cur = (ib - ib_lo) & 1;
+        // this item pair's digit packs of coefficients 8ib + 4h + q (issued before the wait)
+        uint32_t pk[2][4];
+#pragma unroll
+        for (int s = 0; s < 2; s++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) pk[s][q] = (a_row[s][8 * ib + 4 * h + q] + prec) >> (32 - 2 * T);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block ib landed (this thread's pieces), pk loaded
+        __syncthreads();  // every thread's pieces of block ib; every wave done with the other buffer
+        if (ib + 1 < ib_hi) issue(ib + 1, cur ^ 1);
+        const unsigned char *buf = smem + cur * BUF_BYTES;
+#pragma unroll
+        for (int j = 0; j < T; j++) {
+            kg_v4i a[2];
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    a[s][q] = (int)(1u << (8u * ((pk[s][q] >> (2 * (T - 1 - j))) & 3u)));
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const kg_v4i bf = *reinterpret_cast<const kg_v4i *>(buf + j * STEP_BYTES + b * 1024 + lane * 16);
+#pragma unroll
+                for (int s = 0; s < 2; s++) acc[s][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bf, acc[s][b], 0, 0, 0);
+            }
+        }
+    }
+    // partial sums of this K split: part[z][m][w], w < n + 1
+    const int n1 = P.n + 1;
+    uint32_t *pz = part + (size_t)blockIdx.z * B * n1;
+    const int w = 32 * wt + c;
+#pragma unroll
+    for (int s = 0; s < 2; s++)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) {
+            const size_t m = m_base + 32 * s + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const uint32_t val = (uint32_t)acc[s][0][reg] + ((uint32_t)acc[s][1][reg] << 8) +
+                                 ((uint32_t)acc[s][2][reg] << 16) + ((uint32_t)acc[s][3][reg] << 24);
+            if (m < B && w < n1) pz[m * n1 + w] = val;
+        }
+}
+
+// out[m][w] = [w = n]·b_m − Σ_z part[z][m][w] − N·t·128·0x01010101 (mod 2^32)
+__global__ void k_ks_gemm_reduce(KParams P, const uint32_t *__restrict__ lv1, const uint32_t *__restrict__ part,
+                                 uint32_t *__restrict__ out, size_t B, int splits) {
+    const int n1 = P.n + 1;
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= B * n1) return;
+    const size_t m = x / n1;
+    const int w = (int)(x % n1);
+    uint32_t r = (uint32_t)(1024 * P.iks_t) * 128u * 0x01010101u;
+    for (int z = 0; z < splits; z++) r += part[(size_t)z * B * n1 + x];
+    out[x] = (w == P.n ? lv1[m * 1025 + 1024] : 0u) - r;
+}
+
 // Zero the k = 0 rows of a device KSK (left undefined by the reference, key.zig:156).
 __global__ void k_ksk_zero_k0(uint32_t *__restrict__ ksk, int rs, int base, size_t groups) {
     size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3015,9 +3170,48 @@ bool reencrypt_supported(int t_, int basebit) {
            (basebit == 5 && (t_ == 2 || t_ == 3));
 }
 
+// K splits of the gemm form: enough workgroups for one per CU.
+static int ks_gemm_splits(const KParams &P, size_t B) {
+    const size_t tiles = (size_t)(P.n + 1 + 31) / 32 * ((B + KG_ITEMS - 1) / KG_ITEMS);
+    const size_t z = std::max<size_t>(1, device_cus() / tiles);
+    return (int)std::min<size_t>(z, 1024 / 8);
+}
+size_t ks_gemm_part_bytes(const KParams &P, size_t B) { return (size_t)ks_gemm_splits(P, B) * B * (P.n + 1) * 4; }
+
+static hipError_t launch_ks_gemm(const KParams &P, const uint32_t *lv1, const KsGemm &G, uint32_t *out, size_t B,
+                                 hipStream_t s, const char **used) {
+    const int z = ks_gemm_splits(P, B);
+    const int per = (1024 / 8 + z - 1) / z;
+    const int splits = (1024 / 8 + per - 1) / per;
+    dim3 grid((unsigned)((P.n + 1 + 31) / 32), (unsigned)((B + KG_ITEMS - 1) / KG_ITEMS), (unsigned)splits),
+        block(64 * KG_WAVES);
+    switch (P.iks_t) {
+    case 7: hipLaunchKernelGGL((k_key_switch_gemm<7>), grid, block, 0, s, P, lv1, G.kg, G.part, B, per); break;
+    case 8: hipLaunchKernelGGL((k_key_switch_gemm<8>), grid, block, 0, s, P, lv1, G.kg, G.part, B, per); break;
+    case 9: hipLaunchKernelGGL((k_key_switch_gemm<9>), grid, block, 0, s, P, lv1, G.kg, G.part, B, per); break;
+    default: return hipErrorInvalidValue;
+    }
+    const size_t total = B * (size_t)(P.n + 1);
+    hipLaunchKernelGGL(k_ks_gemm_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, P, lv1, G.part, out, B,
+                       splits);
+    if (used) *used = P.iks_t == 9 ? "k_key_switch_gemm<9> + k_ks_gemm_reduce"
+                      : P.iks_t == 8 ? "k_key_switch_gemm<8> + k_ks_gemm_reduce"
+                                     : "k_key_switch_gemm<7> + k_ks_gemm_reduce";
+    return hipGetLastError();
+}
+
+bool ks_gemm_supported(const KParams &P) { return P.basebit == 2 && P.iks_t >= 7 && P.iks_t <= 9; }
+
+hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, hipStream_t s) {
+    const size_t words = ks_gemm_bytes(P) / 4;
+    hipLaunchKernelGGL(k_ksk_to_gemm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, ksk, kg, words);
+    return hipGetLastError();
+}
+
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk, uint32_t *out,
-                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
+                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used, const KsGemm *KG) {
     if (B == 0) return hipSuccess;
+    if (O.ks_form == 2 && KG && KG->kg && KG->part && ks_gemm_supported(P)) return launch_ks_gemm(P, lv1, *KG, out, B, s, used);
     // kernel form: lanes (default) or the select/gather forms (TFHE_OPT_KS_FORM = 1)
     if (O.ks_form == 0 && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s, O, used))
         return hipGetLastError();

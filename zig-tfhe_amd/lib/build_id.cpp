@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "ff7ea4a196060eeb"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "09fac45f4eb4400b"; }
