@@ -92,7 +92,7 @@ def test_key_switch_vs_oracle(oracle, pname, B, form):
     with c.options(ks_form={"sel": 1, "gemm": 2}.get(form, 0), ks_narrow=int(form.endswith("narrow"))):
         assert np.array_equal(c.key_switch(lv1), want)
         if form == "gemm":
-            assert c.last_kernels().startswith("k_key_switch_gemm<") == (pname != "uint4")
+            assert ("k_key_switch_gemm<" in c.last_kernels()) == (pname != "uint4")
 
 
 @pytest.mark.parametrize("B", [1024, 1500])
@@ -105,7 +105,7 @@ def test_key_switch_gemm_full_batches(oracle, B):
     lanes = c.key_switch(lv1)
     with c.options(ks_form=2):
         got = c.key_switch(lv1)
-        assert c.last_kernels().startswith("k_key_switch_gemm<9>")
+        assert "k_key_switch_gemm<9>" in c.last_kernels()
     assert np.array_equal(got, lanes)
     for i in (0, 511, 512, B - 1):
         assert np.array_equal(got[i], oracle.identity_key_switch(k.p, lv1[i], k.ck.ksk))

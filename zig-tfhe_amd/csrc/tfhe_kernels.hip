@@ -2212,9 +2212,9 @@ __global__ __launch_bounds__(256) void k_key_switch_gather(KParams P, const uint
 // permutation is exact).  Workgroup: 8 waves (2 per SIMD), 512 items, one
 // 32-word output tile; wave v takes items 64v..64v+63 as two 32-row MFMA
 // tiles, 2 x 4 accumulators (128 VGPRs).  The B fragments of a coefficient
-// block (t levels x 4 planes x 1 KB) come by LDS-DMA into a double buffer,
-// one barrier per block; K splits over blockIdx.z write partial sums that
-// k_ks_gemm_reduce adds.
+// block (t levels x 4 planes x 1 KB) and the block's input words of the 512
+// items come by LDS-DMA into a 3-slot ring, two blocks ahead, one barrier per
+// block; K splits over blockIdx.z write partial sums that k_ks_gemm_reduce adds.
 constexpr int KG_WAVES = 8;
 constexpr int KG_ITEMS = 64 * KG_WAVES;  // items per workgroup
 typedef int kg_v4i __attribute__((ext_vector_type(4)));
@@ -2248,38 +2248,55 @@ __global__ void k_ksk_to_gemm(KParams P, const uint32_t *__restrict__ ksk, uint3
     kg[x] = v;
 }
 
+// s_waitcnt vmcnt(N) for the ring's two wave kinds (an immediate per case).
+template <int N>
+DEV void kg_wait() {
+    static_assert(N == 0 || N == 2 || (N >= 9 && N <= 11), "kg_wait");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+}
+
 template <int T>
 __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P, const uint32_t *__restrict__ lv1,
                                                                    const uint32_t *__restrict__ kg,
                                                                    uint32_t *__restrict__ part, size_t B,
                                                                    int ib_per_split) {
-    constexpr int STEP_BYTES = 4 * 1024;  // one level's 4 planes of one 32-word tile
-    constexpr int BUF_BYTES = T * STEP_BYTES;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES];
+    constexpr int STEP_BYTES = 4 * 1024;                 // one level's 4 planes of one 32-word tile
+    constexpr int WORDS_BYTES = 8 * KG_ITEMS * 4;        // the block's 8 input words of the 512 items
+    constexpr int BUF_BYTES = T * STEP_BYTES + WORDS_BYTES;
+    constexpr int STAGES = 3;                            // blocks ib (read), ib + 1 (landing), ib + 2 (issued)
+    static_assert(STAGES * BUF_BYTES <= 160 * 1024, "gemm key-switch LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * BUF_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int v = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool loader = v < 4;  // waves 0-3 also issue the KSK pieces: 4 KB per level, 256 threads x 16 B
     const int w32 = (P.n + 1 + 31) / 32;
     const int wt = blockIdx.x;
     const int ib_lo = blockIdx.z * ib_per_split, ib_hi = min(1024 / 8, ib_lo + ib_per_split);
-    const size_t m_base = (size_t)blockIdx.y * KG_ITEMS + 64 * v;
+    const size_t m_wg = (size_t)blockIdx.y * KG_ITEMS;
     const int h = lane >> 5, c = lane & 31;
-    // this lane's two items (rows c of the wave's two MFMA tiles), clamped
-    const uint32_t *a_row[2];
+    // the block's 8 input words of item 256r + tid/2, half tid & 1 (16 B), r = 0, 1
+    const uint32_t *a_src[2];
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
-        const size_t m = m_base + 32 * s + c;
-        a_row[s] = lv1 + (m < B ? m : B - 1) * 1025;
+    for (int r = 0; r < 2; r++) {
+        const size_t m = m_wg + 256 * r + (tid >> 1);
+        a_src[r] = lv1 + (m < B ? m : B - 1) * 1025 + 4 * (tid & 1);
     }
-    // DMA of coefficient block ib: T x 4 KB, 512 threads x 16 B x (T/2 rounded up) ... one
-    // 16-B piece per thread per 8 KB: level pairs
     const uint32_t lds0 = (uint32_t)(size_t)(lds_void_t *)smem;
-    auto issue = [&](int ib, int which) {
+    // In flight per wave, oldest first: block ib's pieces, then block ib + 1's
+    // (loader waves T + 2 per block, the others 2), all by LDS-DMA: no VGPR
+    // holds a load in flight, so the only waits are the kg_wait below.
+    auto issue = [&](int ib, int slot) {
+        const uint32_t base = lds0 + slot * BUF_BYTES;
+        if (loader) {
 #pragma unroll
-        for (int j = 0; j < T; j++) {
-            if (tid < 256) {  // 4 KB per level: 256 threads x 16 B
-                const uint32_t *src = kg + ((((size_t)j * (1024 / 8) + ib) * w32 + wt) * 1024 + tid * 16) / 4;
-                const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + which * BUF_BYTES + j * STEP_BYTES +
-                                                                    (tid & ~63) * 16);
+            for (int j = 0; j < T; j++) {
+                // block (j, ib, wt) is 4 KB = 1,024 words; thread tid's 16 B at word 4 tid
+                const uint32_t *src = kg + (((size_t)j * (1024 / 8) + ib) * w32 + wt) * 1024 + tid * 4;
+                const uint32_t dst = __builtin_amdgcn_readfirstlane(base + j * STEP_BYTES + (tid & ~63) * 16);
                 uint32_t keep;
                 asm volatile(
                     "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -2287,6 +2304,17 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
                     : "v"(src), "s"(dst)
                     : "memory");
             }
+        }
+#pragma unroll
+        for (int r = 0; r < 2; r++) {  // words [item][8]: 16 B per lane, item 256r + tid/2
+            const uint32_t dst =
+                __builtin_amdgcn_readfirstlane(base + T * STEP_BYTES + r * 256 * 32 + (tid & ~63) * 16);
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(a_src[r] + 8 * ib), "s"(dst)
+                : "memory");
         }
     };
     kg_v16i acc[2][4];
@@ -2296,18 +2324,26 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
         for (int b = 0; b < 4; b++) acc[s][b] = kg_v16i{};
     const uint32_t prec = 1u << (32 - (1 + 2 * T));
     if (ib_lo < ib_hi) issue(ib_lo, 0);
+    if (ib_lo + 1 < ib_hi) issue(ib_lo + 1, 1);
     for (int ib = ib_lo; ib < ib_hi; ib++) {
-        const int cur = (ib - ib_lo) & 1;
-        // this item pair's digit packs of coefficients 8ib + 4h + q (issued before the wait)
+        const int slot = (ib - ib_lo) % STAGES;
+        if (ib + 1 < ib_hi) {  // block ib + 1 may stay in flight
+            if (loader) kg_wait<T + 2>();
+            else kg_wait<2>();
+        } else {
+            kg_wait<0>();
+        }
+        __syncthreads();  // block ib landed for every wave; every wave done with block ib - 1
+        if (ib + 2 < ib_hi) issue(ib + 2, (slot + 2) % STAGES);  // into block ib - 1's slot
+        const unsigned char *buf = smem + slot * BUF_BYTES;
+        const uint32_t *words = reinterpret_cast<const uint32_t *>(buf + T * STEP_BYTES);
         uint32_t pk[2][4];
 #pragma unroll
-        for (int s = 0; s < 2; s++)
+        for (int s = 0; s < 2; s++) {
+            const kg_v4i wv = *reinterpret_cast<const kg_v4i *>(words + (64 * v + 32 * s + c) * 8 + 4 * h);
 #pragma unroll
-            for (int q = 0; q < 4; q++) pk[s][q] = (a_row[s][8 * ib + 4 * h + q] + prec) >> (32 - 2 * T);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block ib landed (this thread's pieces), pk loaded
-        __syncthreads();  // every thread's pieces of block ib; every wave done with the other buffer
-        if (ib + 1 < ib_hi) issue(ib + 1, cur ^ 1);
-        const unsigned char *buf = smem + cur * BUF_BYTES;
+            for (int q = 0; q < 4; q++) pk[s][q] = ((uint32_t)wv[q] + prec) >> (32 - 2 * T);
+        }
 #pragma unroll
         for (int j = 0; j < T; j++) {
             kg_v4i a[2];
@@ -2328,6 +2364,7 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
     const int n1 = P.n + 1;
     uint32_t *pz = part + (size_t)blockIdx.z * B * n1;
     const int w = 32 * wt + c;
+    const size_t m_base = m_wg + 64 * v;
 #pragma unroll
     for (int s = 0; s < 2; s++)
 #pragma unroll

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "09fac45f4eb4400b"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "6f42bccc38c84f34"; }
