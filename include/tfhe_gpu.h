@@ -132,8 +132,10 @@ enum {
     TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 2 split, 3 latency, 4 pair,
                                      5 octo (8 items per workgroup, two gate waves per SIMD) */
     TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
-    TFHE_OPT_KS_FORM = 3,         /* key switch: 0 lanes (default), 1 select / gather, 2 one-hot
-                                     GEMM on the matrix cores (basebit 2; others fall back to lanes) */
+    TFHE_OPT_KS_FORM = 3,         /* key switch: 3 auto (default: the one-hot GEMM on the matrix
+                                     cores for basebit 2, else lanes), 0 lanes,
+                                     1 select / gather, 2 the GEMM at any batch (basebit 2; other
+                                     parameter sets fall back to lanes) */
     TFHE_OPT_KS_NARROW = 4,       /* basebit 2: 0 auto (default), 1 32-word x 4-wave blocks */
     TFHE_OPT_KS_ITEM_GROUPS = 5,  /* basebit >= 5: 0 auto (above 64 items the ring form: 4 item groups
                                      share a 4-deep DMA ring), 1, 2, 4, 8 forces the lane form with

@@ -530,8 +530,8 @@ def test_fused_and_reference_arithmetic_agree_1024(oracle):
 
 def test_options_validation_and_report(oracle):
     """tfhe_gpu_set_option rejects unknown keys / values; the last-kernel report
-    names the default forms (loader-wave whole form + the wide lane key switch at 1,024
-    gates, the latency form below 512)."""
+    names the default forms (the latency form below 512 items, the one-hot GEMM key
+    switch; the lane key switch under ks_form = 0)."""
     c, k = ctx_for(oracle, "128")
     with pytest.raises(tfhe_amd.TfheError):
         c.set_option("br_form", 9)
@@ -540,10 +540,14 @@ def test_options_validation_and_report(oracle):
     g = rng(91)
     cts = u32rand(g, 3, k.p.n + 1)
     c.bootstrap_batch(cts)
-    assert c.last_kernels() == "k_blind_rotate_wide<3,true,true> (latency form, fused) + k_key_switch_lanes<9,2,32,4,1>"
+    gemm = "k_key_switch_gemm<9> + k_ks_gemm_reduce"
+    assert c.last_kernels() == "k_blind_rotate_wide<3,true,true> (latency form, fused) + " + gemm
     with c.options(arith=tfhe_amd.ARITH_REFERENCE):
         c.bootstrap_batch(cts)
-        assert c.last_kernels() == "k_blind_rotate_wide<3,true,false> (latency form) + k_key_switch_lanes<9,2,32,4,1>"
+        assert c.last_kernels() == "k_blind_rotate_wide<3,true,false> (latency form) + " + gemm
+    with c.options(ks_form=0):
+        c.bootstrap_batch(cts)
+        assert c.last_kernels().endswith("k_key_switch_lanes<9,2,32,4,1>")
 
 
 def test_slot_counters_and_barrier_agree_at_full_size(oracle):

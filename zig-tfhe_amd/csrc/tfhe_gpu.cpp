@@ -241,12 +241,14 @@ enum RunKind : int {
     RUN_NO_KEYSWITCH = 2,  // sampleExtractIndex2, n+1 words (vanilla.zig:58-69)
 };
 
-// The gemm key switch's buffers for a batch of B (TFHE_OPT_KS_FORM = 2): the
+// The gemm key switch's buffers for a batch of B (TFHE_OPT_KS_FORM = 2, or 3 from
+// KS_GEMM_MIN_ITEMS items): the
 // MFMA-layout KSK, rebuilt on the stream after a key change, and the partial
 // sums.  G stays empty for the other forms (launch_key_switch ignores it).
 int ks_gemm_args(tfhe_gpu_ctx *c, size_t B, KsGemm &G) {
     G = KsGemm();
-    if (c->opts.ks_form != 2 || !ks_gemm_supported(c->K)) return TFHE_OK;
+    if ((c->opts.ks_form != 2 && (c->opts.ks_form != 3 || B < KS_GEMM_MIN_ITEMS)) || !ks_gemm_supported(c->K))
+        return TFHE_OK;
     if (!c->d_ksk_gemm) {
         hipError_t e = hipMalloc((void **)&c->d_ksk_gemm, ks_gemm_bytes(c->K));
         if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, "hipMalloc(ksk gemm layout)");
@@ -1589,7 +1591,7 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     bool ok = false;
     switch (key) {
     case TFHE_OPT_BR_FORM: ok = v >= 0 && v <= 5; break;
-    case TFHE_OPT_KS_FORM: ok = v >= 0 && v <= 2; break;
+    case TFHE_OPT_KS_FORM: ok = v >= 0 && v <= 3; break;
     case TFHE_OPT_BR_LOADER:
     case TFHE_OPT_KS_NARROW:
     case TFHE_OPT_CIRCUIT_PACK:

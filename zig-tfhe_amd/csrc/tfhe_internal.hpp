@@ -77,7 +77,7 @@ struct LaunchOpts {
     int br_form = 0;     // 0 auto, 1 whole, 2 split, 3 latency (wide), 4 pair
     int br_loader = 1;   // whole form: 1 loader waves issue the BK DMAs, 0 the gate waves do
     int br_flags = 1;    // whole form with loader waves: 1 slot counters (default), 0 a barrier per row pair
-    int ks_form = 0;     // 0 lanes, 1 select / gather, 2 one-hot GEMM on the matrix cores (basebit 2)
+    int ks_form = 3;     // 0 lanes, 1 select / gather, 2 one-hot GEMM on the matrix cores (basebit 2), 3 auto
     int ks_narrow = 0;   // basebit 2: 1 forces the 32-word x 4-wave blocks
     int ks_groups = 0;   // basebit >= 5: item groups per block (0 auto = 4; 1, 2, 4, 8)
     int ks_sel_items = 8;  // select/gather form: items per block (8, 16, 32)
@@ -110,6 +110,7 @@ struct KsGemm {
 size_t ks_gemm_bytes(const KParams &P);
 size_t ks_gemm_part_bytes(const KParams &P, size_t B);
 bool ks_gemm_supported(const KParams &P);
+extern size_t KS_GEMM_MIN_ITEMS;
 hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, hipStream_t s);
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
                              uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),

@@ -3238,6 +3238,11 @@ static hipError_t launch_ks_gemm(const KParams &P, const uint32_t *lv1, const Ks
 }
 
 bool ks_gemm_supported(const KParams &P) { return P.basebit == 2 && P.iks_t >= 7 && P.iks_t <= 9; }
+// Batches from this size take the GEMM under TFHE_OPT_KS_FORM = 3: it is the
+// faster form from 64 items up (0.050 vs 0.218 ms at 64, 0.090 vs 0.239 ms at
+// 1,024, 0.35 vs 0.94 ms at 4,096; profiles/r03k_ks_gemm.txt), and a batch of
+// one still fills 242 workgroups (22 tiles x 11 K splits).
+size_t KS_GEMM_MIN_ITEMS = 1;
 
 hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, hipStream_t s) {
     const size_t words = ks_gemm_bytes(P) / 4;
@@ -3248,9 +3253,13 @@ hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *k
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk, uint32_t *out,
                              size_t B, hipStream_t s, const LaunchOpts &O, const char **used, const KsGemm *KG) {
     if (B == 0) return hipSuccess;
-    if (O.ks_form == 2 && KG && KG->kg && KG->part && ks_gemm_supported(P)) return launch_ks_gemm(P, lv1, *KG, out, B, s, used);
-    // kernel form: lanes (default) or the select/gather forms (TFHE_OPT_KS_FORM = 1)
-    if (O.ks_form == 0 && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s, O, used))
+    // kernel form (TFHE_OPT_KS_FORM): 3 auto (default) = the one-hot GEMM for
+    // basebit 2 from KS_GEMM_MIN_ITEMS items, else lanes; 2 the GEMM wherever it
+    // applies; 0 lanes; 1 the select / gather forms
+    const bool gemm_ok = KG && KG->kg && KG->part && ks_gemm_supported(P);
+    if (gemm_ok && (O.ks_form == 2 || (O.ks_form == 3 && B >= KS_GEMM_MIN_ITEMS)))
+        return launch_ks_gemm(P, lv1, *KG, out, B, s, used);
+    if (O.ks_form != 1 && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s, O, used))
         return hipGetLastError();
     // items per block: TFHE_OPT_KS_SEL_ITEMS in {8, 16, 32} (default 8)
     const int G = (O.ks_sel_items == 16 || O.ks_sel_items == 32) ? O.ks_sel_items : 8;

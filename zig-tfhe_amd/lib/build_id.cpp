@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "6f42bccc38c84f34"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "b9b3cb35de6e928c"; }
