@@ -193,6 +193,26 @@ def test_gpu_reencrypt_matches_oracle(oracle, P, keys, reenc_ab):
 
 
 @pytest.mark.gpu
+def test_gpu_reencrypt_gemm_and_lanes_agree(oracle, P, keys, reenc_ab):
+    """The one-hot GEMM key switch (the default at basebit 2)
+    over the n = 700 input coefficients (88 blocks of 8, the last half padding)
+    against the lane form, bit for bit, and the oracle on samples."""
+    ctx = tfhe_amd.Context(N128, device=0)
+    hr = tfhe_amd.HipReencryptor(ctx, tfhe_amd.ProxyReencryptionKey(reenc_ab, P.basebit, P.iks_t))
+    x = _random_cts(P, 1500, 1500)
+    g = hr.reencrypt(x)
+    assert "k_key_switch_gemm<9>" in ctx.last_kernels()
+    with ctx.options(ks_form=0):
+        lanes = hr.reencrypt(x)
+        assert "k_key_switch_lanes<" in ctx.last_kernels()
+    assert np.array_equal(g, lanes)
+    for i in (0, 511, 512, 1499):
+        assert np.array_equal(g[i], oracle.reencrypt(P.n, P.basebit, P.iks_t, x[i], reenc_ab)), i
+    hr.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pname,basebit,t", [("80", 2, 7), ("128", 4, 4), ("uint4", 5, 3)])
 def test_gpu_reencrypt_other_bases(oracle, pname, basebit, t):
     from oracle import params

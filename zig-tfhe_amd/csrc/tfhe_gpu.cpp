@@ -250,14 +250,14 @@ int ks_gemm_args(tfhe_gpu_ctx *c, size_t B, KsGemm &G) {
     if ((c->opts.ks_form != 2 && (c->opts.ks_form != 3 || B < KS_GEMM_MIN_ITEMS)) || !ks_gemm_supported(c->K))
         return TFHE_OK;
     if (!c->d_ksk_gemm) {
-        hipError_t e = hipMalloc((void **)&c->d_ksk_gemm, ks_gemm_bytes(c->K));
+        hipError_t e = hipMalloc((void **)&c->d_ksk_gemm, ks_gemm_bytes(c->K, 1024, c->K.iks_t));
         if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, "hipMalloc(ksk gemm layout)");
     }
     if (!c->ksk_gemm_ok) {
-        HIPCHK(c, launch_ksk_to_gemm(c->K, c->d_ksk, c->d_ksk_gemm, c->stream));
+        HIPCHK(c, launch_ksk_to_gemm(c->K, c->d_ksk, c->d_ksk_gemm, 1024, c->K.iks_t, c->stream));
         c->ksk_gemm_ok = true;
     }
-    int rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B));
+    int rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B, 1024));
     if (rc) return rc;
     G.kg = c->d_ksk_gemm;
     G.part = (uint32_t *)c->s_kspart.p;
@@ -1053,6 +1053,7 @@ struct tfhe_gpu_reenc_key {
     int device = 0;
     uint32_t basebit = 0, t = 0;
     uint32_t *d_key = nullptr;  // padded rows like the KSK (K.ks_stride words) + zero tail
+    uint32_t *d_key_gemm = nullptr;  // the gemm key switch's layout of d_key (basebit 2, t 7..9), or NULL
     std::vector<tfhe_gpu_reenc_key *> peers;  // multi-device context: the copy on shard k is peers[k - 1]
 };
 
@@ -1081,9 +1082,14 @@ static int reenc_key_load_one(tfhe_gpu_ctx *c, const uint32_t *key_encryptions, 
         e = hipMemcpy2DAsync(k->d_key, stride * 4, key_encryptions, (n + 1) * 4, (n + 1) * 4, rows,
                              hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_key_zero_k0(c->K, k->d_key, (int)n, (int)t, (int)basebit, c->stream);
+    if (e == hipSuccess && ks_gemm_supported((int)t, (int)basebit)) {  // §4.4b layout for the gemm form
+        e = hipMalloc((void **)&k->d_key_gemm, ks_gemm_bytes(c->K, (int)n, (int)t));
+        if (e == hipSuccess) e = launch_ksk_to_gemm(c->K, k->d_key, k->d_key_gemm, (int)n, (int)t, c->stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         (void)hipFree(k->d_key);
+        if (k->d_key_gemm) (void)hipFree(k->d_key_gemm);
         delete k;
         return hip_fail(c, e, "upload reencryption key");
     }
@@ -1096,6 +1102,7 @@ void tfhe_gpu_reenc_key_destroy(tfhe_gpu_reenc_key *k) {
     for (tfhe_gpu_reenc_key *p : k->peers) tfhe_gpu_reenc_key_destroy(p);
     (void)hipSetDevice(k->device);
     (void)hipFree(k->d_key);
+    if (k->d_key_gemm) (void)hipFree(k->d_key_gemm);
     delete k;
 }
 
@@ -1106,11 +1113,19 @@ static int reencrypt_batch_one(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, con
     if (B == 0) return TFHE_OK;
     HIPCHK(c, hipSetDevice(c->device));
     const size_t w = tlwe0_words(c);
-    int rc = h2d(c, c->s_a, in, B * w * 4);
+    int rc = ensure(c, c->s_a, B * w * 4 + KS_GEMM_INPUT_SLACK);  // the gemm form reads whole blocks of 8
+    if (!rc) rc = h2d(c, c->s_a, in, B * w * 4);
     if (!rc) rc = ensure(c, c->s_out, B * w * 4);
     if (rc) return rc;
+    KsGemm G;
+    if (k->d_key_gemm) {
+        rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B, (int)c->P.n));
+        if (rc) return rc;
+        G.kg = k->d_key_gemm;
+        G.part = (uint32_t *)c->s_kspart.p;
+    }
     HIPCHK(c, launch_reencrypt(c->K, (int)k->t, (int)k->basebit, (const uint32_t *)c->s_a.p, k->d_key,
-                               (uint32_t *)c->s_out.p, B, c->stream, c->opts, &c->last_ks));
+                               (uint32_t *)c->s_out.p, B, c->stream, c->opts, &c->last_ks, &G));
     return d2h_sync(c, out, c->s_out.p, B * w * 4);
 }
 

@@ -107,11 +107,15 @@ struct KsGemm {
     const uint32_t *kg = nullptr;
     uint32_t *part = nullptr;
 };
-size_t ks_gemm_bytes(const KParams &P);
-size_t ks_gemm_part_bytes(const KParams &P, size_t B);
+// n_in: input coefficients (1024 for the identity key switch, n for a proxy
+// re-encryption key); t levels of basebit 2
+size_t ks_gemm_bytes(const KParams &P, int n_in, int t);
+size_t ks_gemm_part_bytes(const KParams &P, size_t B, int n_in);
 bool ks_gemm_supported(const KParams &P);
+bool ks_gemm_supported(int t, int basebit);
 extern size_t KS_GEMM_MIN_ITEMS;
-hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, hipStream_t s);
+constexpr size_t KS_GEMM_INPUT_SLACK = 16;  // bytes past the last input row the gemm form may read
+hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, int n_in, int t, hipStream_t s);
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
                              uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),
                              const char **used = nullptr, const KsGemm *G = nullptr);
@@ -123,7 +127,7 @@ hipError_t launch_key_zero_k0(const KParams &P, uint32_t *key, int n_in, int t, 
 // rows in the padded device layout; in/out B TLWELv0
 hipError_t launch_reencrypt(const KParams &P, int t, int basebit, const uint32_t *in, const uint32_t *key,
                             uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),
-                            const char **used = nullptr);
+                            const char **used = nullptr, const KsGemm *G = nullptr);
 bool reencrypt_supported(int t, int basebit);
 hipError_t launch_fft_forward(const DevTables &T, const uint32_t *in, double *out, size_t B,
                               hipStream_t s);

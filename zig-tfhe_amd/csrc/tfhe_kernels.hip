@@ -2223,26 +2223,30 @@ typedef int kg_v16i __attribute__((ext_vector_type(16)));
 // MFMA-layout KSK, built from the device KSK (k = 0 rows zeroed):
 // kg[j][ib][wt][b][lane][e] int8, lane = 32h + c: byte b of
 // KSK[i = 8ib + 4h + (e >> 2)][j][k = e & 3][w = 32wt + c] − 128 (w > n: 0 − 128).
-size_t ks_gemm_bytes(const KParams &P) {
+// n_in input coefficients (N for the identity key switch, n for the proxy
+// re-encryption key) in blocks of 8: coefficients past n_in select zero rows.
+__host__ __device__ __forceinline__ int kg_blocks(int n_in) { return (n_in + 7) / 8; }
+size_t ks_gemm_bytes(const KParams &P, int n_in, int t) {
     const size_t w32 = (size_t)(P.n + 1 + 31) / 32;
-    return (size_t)P.iks_t * (1024 / 8) * w32 * 4 * 1024;
+    return (size_t)t * kg_blocks(n_in) * w32 * 4 * 1024;
 }
-__global__ void k_ksk_to_gemm(KParams P, const uint32_t *__restrict__ ksk, uint32_t *__restrict__ kg, size_t words) {
+__global__ void k_ksk_to_gemm(KParams P, const uint32_t *__restrict__ ksk, uint32_t *__restrict__ kg, size_t words,
+                              int n_in, int t) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // one u32 = bytes e = 4q .. 4q+3
     if (x >= words) return;
-    const int w32 = (P.n + 1 + 31) / 32;
+    const int w32 = (P.n + 1 + 31) / 32, nib = kg_blocks(n_in);
     const int q = (int)(x & 3), lane = (int)((x >> 2) & 63), b = (int)((x >> 8) & 3);
     size_t r = x >> 10;
     const int wt = (int)(r % w32);
     r /= w32;
-    const int ib = (int)(r % (1024 / 8)), j = (int)(r / (1024 / 8));
+    const int ib = (int)(r % nib), j = (int)(r / nib);
     const int h = lane >> 5, c = lane & 31;
     const int i = 8 * ib + 4 * h + q, w = 32 * wt + c;
     const size_t rs = (size_t)P.ks_stride;
     uint32_t v = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const uint32_t word = w <= P.n ? ksk[((size_t)(4 * P.iks_t) * i + 4 * j + k) * rs + w] : 0u;
+        const uint32_t word = (w <= P.n && i < n_in) ? ksk[((size_t)(4 * t) * i + 4 * j + k) * rs + w] : 0u;
         v |= (((word >> (8 * b)) & 255u) ^ 128u) << (8 * k);  // byte − 128 as int8
     }
     kg[x] = v;
@@ -2263,7 +2267,7 @@ template <int T>
 __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P, const uint32_t *__restrict__ lv1,
                                                                    const uint32_t *__restrict__ kg,
                                                                    uint32_t *__restrict__ part, size_t B,
-                                                                   int ib_per_split) {
+                                                                   int ib_per_split, int n_in, int in_stride) {
     constexpr int STEP_BYTES = 4 * 1024;                 // one level's 4 planes of one 32-word tile
     constexpr int WORDS_BYTES = 8 * KG_ITEMS * 4;        // the block's 8 input words of the 512 items
     constexpr int BUF_BYTES = T * STEP_BYTES + WORDS_BYTES;
@@ -2275,7 +2279,8 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
     const bool loader = v < 4;  // waves 0-3 also issue the KSK pieces: 4 KB per level, 256 threads x 16 B
     const int w32 = (P.n + 1 + 31) / 32;
     const int wt = blockIdx.x;
-    const int ib_lo = blockIdx.z * ib_per_split, ib_hi = min(1024 / 8, ib_lo + ib_per_split);
+    const int nib = kg_blocks(n_in);
+    const int ib_lo = blockIdx.z * ib_per_split, ib_hi = min(nib, ib_lo + ib_per_split);
     const size_t m_wg = (size_t)blockIdx.y * KG_ITEMS;
     const int h = lane >> 5, c = lane & 31;
     // the block's 8 input words of item 256r + tid/2, half tid & 1 (16 B), r = 0, 1
@@ -2283,7 +2288,7 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         const size_t m = m_wg + 256 * r + (tid >> 1);
-        a_src[r] = lv1 + (m < B ? m : B - 1) * 1025 + 4 * (tid & 1);
+        a_src[r] = lv1 + (m < B ? m : B - 1) * (size_t)in_stride;
     }
     const uint32_t lds0 = (uint32_t)(size_t)(lds_void_t *)smem;
     // In flight per wave, oldest first: block ib's pieces, then block ib + 1's
@@ -2295,7 +2300,7 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
 #pragma unroll
             for (int j = 0; j < T; j++) {
                 // block (j, ib, wt) is 4 KB = 1,024 words; thread tid's 16 B at word 4 tid
-                const uint32_t *src = kg + (((size_t)j * (1024 / 8) + ib) * w32 + wt) * 1024 + tid * 4;
+                const uint32_t *src = kg + (((size_t)j * nib + ib) * w32 + wt) * 1024 + tid * 4;
                 const uint32_t dst = __builtin_amdgcn_readfirstlane(base + j * STEP_BYTES + (tid & ~63) * 16);
                 uint32_t keep;
                 asm volatile(
@@ -2305,15 +2310,19 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
                     : "memory");
             }
         }
+        // words [item][8]: 16 B per lane, item 256r + tid/2.  Coefficients past
+        // n_in select zero rows, so what a block's last words read there (the next
+        // row, or the caller's slack past the last one: launch_ks_gemm) is unused.
+        const int off_ok = 8 * ib + 4 * (tid & 1);
 #pragma unroll
-        for (int r = 0; r < 2; r++) {  // words [item][8]: 16 B per lane, item 256r + tid/2
+        for (int r = 0; r < 2; r++) {
             const uint32_t dst =
                 __builtin_amdgcn_readfirstlane(base + T * STEP_BYTES + r * 256 * 32 + (tid & ~63) * 16);
             uint32_t keep;
             asm volatile(
                 "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                 : "=&s"(keep)
-                : "v"(a_src[r] + 8 * ib), "s"(dst)
+                : "v"(a_src[r] + off_ok), "s"(dst)
                 : "memory");
         }
     };
@@ -2376,17 +2385,17 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
         }
 }
 
-// out[m][w] = [w = n]·b_m − Σ_z part[z][m][w] − N·t·128·0x01010101 (mod 2^32)
+// out[m][w] = [w = n]·b_m − Σ_z part[z][m][w] − 8·blocks·t·128·0x01010101 (mod 2^32)
 __global__ void k_ks_gemm_reduce(KParams P, const uint32_t *__restrict__ lv1, const uint32_t *__restrict__ part,
-                                 uint32_t *__restrict__ out, size_t B, int splits) {
+                                 uint32_t *__restrict__ out, size_t B, int splits, int n_in, int in_stride, int t) {
     const int n1 = P.n + 1;
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= B * n1) return;
     const size_t m = x / n1;
     const int w = (int)(x % n1);
-    uint32_t r = (uint32_t)(1024 * P.iks_t) * 128u * 0x01010101u;
+    uint32_t r = (uint32_t)(8 * kg_blocks(n_in) * t) * 128u * 0x01010101u;
     for (int z = 0; z < splits; z++) r += part[(size_t)z * B * n1 + x];
-    out[x] = (w == P.n ? lv1[m * 1025 + 1024] : 0u) - r;
+    out[x] = (w == P.n ? lv1[m * (size_t)in_stride + n_in] : 0u) - r;
 }
 
 // Zero the k = 0 rows of a device KSK (left undefined by the reference, key.zig:156).
@@ -3195,9 +3204,15 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
     return true;
 }
 
+static hipError_t launch_ks_gemm(const KParams &P, int t, int n_in, int in_stride, const uint32_t *in,
+                                 const KsGemm &G, uint32_t *out, size_t B, hipStream_t s, const char **used);
+
 hipError_t launch_reencrypt(const KParams &P, int t_, int basebit, const uint32_t *in, const uint32_t *key,
-                            uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
+                            uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O, const char **used,
+                            const KsGemm *KG) {
     if (B == 0) return hipSuccess;
+    if (KG && KG->kg && KG->part && ks_gemm_supported(t_, basebit) && (O.ks_form == 2 || O.ks_form == 3))
+        return launch_ks_gemm(P, t_, P.n, P.n + 1, in, *KG, out, B, s, used);
     if (!launch_ks_lanes(P, t_, basebit, in, P.n, P.n + 1, key, out, B, s, O, used)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
@@ -3208,45 +3223,53 @@ bool reencrypt_supported(int t_, int basebit) {
 }
 
 // K splits of the gemm form: enough workgroups for one per CU.
-static int ks_gemm_splits(const KParams &P, size_t B) {
+static int ks_gemm_splits(const KParams &P, size_t B, int n_in) {
     const size_t tiles = (size_t)(P.n + 1 + 31) / 32 * ((B + KG_ITEMS - 1) / KG_ITEMS);
     const size_t z = std::max<size_t>(1, device_cus() / tiles);
-    return (int)std::min<size_t>(z, 1024 / 8);
+    return (int)std::min<size_t>(z, (size_t)kg_blocks(n_in));
 }
-size_t ks_gemm_part_bytes(const KParams &P, size_t B) { return (size_t)ks_gemm_splits(P, B) * B * (P.n + 1) * 4; }
+size_t ks_gemm_part_bytes(const KParams &P, size_t B, int n_in) {
+    return (size_t)ks_gemm_splits(P, B, n_in) * B * (P.n + 1) * 4;
+}
 
-static hipError_t launch_ks_gemm(const KParams &P, const uint32_t *lv1, const KsGemm &G, uint32_t *out, size_t B,
-                                 hipStream_t s, const char **used) {
-    const int z = ks_gemm_splits(P, B);
-    const int per = (1024 / 8 + z - 1) / z;
-    const int splits = (1024 / 8 + per - 1) / per;
+// One-hot GEMM key switch of B inputs of in_stride words (n_in coefficients, then b)
+// against a MFMA-layout key of t levels (ks_gemm_supported).  The kernel reads
+// whole blocks of 8 coefficients: when 8·ceil(n_in/8) > in_stride, the input
+// buffer needs 16 readable bytes past its last row (KS_GEMM_INPUT_SLACK).
+static hipError_t launch_ks_gemm(const KParams &P, int t, int n_in, int in_stride, const uint32_t *in,
+                                 const KsGemm &G, uint32_t *out, size_t B, hipStream_t s, const char **used) {
+    const int nib = kg_blocks(n_in);
+    const int z = ks_gemm_splits(P, B, n_in);
+    const int per = (nib + z - 1) / z;
+    const int splits = (nib + per - 1) / per;
     dim3 grid((unsigned)((P.n + 1 + 31) / 32), (unsigned)((B + KG_ITEMS - 1) / KG_ITEMS), (unsigned)splits),
         block(64 * KG_WAVES);
-    switch (P.iks_t) {
-    case 7: hipLaunchKernelGGL((k_key_switch_gemm<7>), grid, block, 0, s, P, lv1, G.kg, G.part, B, per); break;
-    case 8: hipLaunchKernelGGL((k_key_switch_gemm<8>), grid, block, 0, s, P, lv1, G.kg, G.part, B, per); break;
-    case 9: hipLaunchKernelGGL((k_key_switch_gemm<9>), grid, block, 0, s, P, lv1, G.kg, G.part, B, per); break;
+    switch (t) {
+    case 7: hipLaunchKernelGGL((k_key_switch_gemm<7>), grid, block, 0, s, P, in, G.kg, G.part, B, per, n_in, in_stride); break;
+    case 8: hipLaunchKernelGGL((k_key_switch_gemm<8>), grid, block, 0, s, P, in, G.kg, G.part, B, per, n_in, in_stride); break;
+    case 9: hipLaunchKernelGGL((k_key_switch_gemm<9>), grid, block, 0, s, P, in, G.kg, G.part, B, per, n_in, in_stride); break;
     default: return hipErrorInvalidValue;
     }
     const size_t total = B * (size_t)(P.n + 1);
-    hipLaunchKernelGGL(k_ks_gemm_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, P, lv1, G.part, out, B,
-                       splits);
-    if (used) *used = P.iks_t == 9 ? "k_key_switch_gemm<9> + k_ks_gemm_reduce"
-                      : P.iks_t == 8 ? "k_key_switch_gemm<8> + k_ks_gemm_reduce"
-                                     : "k_key_switch_gemm<7> + k_ks_gemm_reduce";
+    hipLaunchKernelGGL(k_ks_gemm_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, P, in, G.part, out, B,
+                       splits, n_in, in_stride, t);
+    if (used) *used = t == 9 ? "k_key_switch_gemm<9> + k_ks_gemm_reduce"
+                      : t == 8 ? "k_key_switch_gemm<8> + k_ks_gemm_reduce"
+                               : "k_key_switch_gemm<7> + k_ks_gemm_reduce";
     return hipGetLastError();
 }
 
-bool ks_gemm_supported(const KParams &P) { return P.basebit == 2 && P.iks_t >= 7 && P.iks_t <= 9; }
+bool ks_gemm_supported(int t, int basebit) { return basebit == 2 && t >= 7 && t <= 9; }
+bool ks_gemm_supported(const KParams &P) { return ks_gemm_supported(P.iks_t, P.basebit); }
 // Batches from this size take the GEMM under TFHE_OPT_KS_FORM = 3: it is the
 // faster form from 64 items up (0.050 vs 0.218 ms at 64, 0.090 vs 0.239 ms at
 // 1,024, 0.35 vs 0.94 ms at 4,096; profiles/r03k_ks_gemm.txt), and a batch of
 // one still fills 242 workgroups (22 tiles x 11 K splits).
 size_t KS_GEMM_MIN_ITEMS = 1;
 
-hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, hipStream_t s) {
-    const size_t words = ks_gemm_bytes(P) / 4;
-    hipLaunchKernelGGL(k_ksk_to_gemm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, ksk, kg, words);
+hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, int n_in, int t, hipStream_t s) {
+    const size_t words = ks_gemm_bytes(P, n_in, t) / 4;
+    hipLaunchKernelGGL(k_ksk_to_gemm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, ksk, kg, words, n_in, t);
     return hipGetLastError();
 }
 
@@ -3258,7 +3281,7 @@ hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32
     // applies; 0 lanes; 1 the select / gather forms
     const bool gemm_ok = KG && KG->kg && KG->part && ks_gemm_supported(P);
     if (gemm_ok && (O.ks_form == 2 || (O.ks_form == 3 && B >= KS_GEMM_MIN_ITEMS)))
-        return launch_ks_gemm(P, lv1, *KG, out, B, s, used);
+        return launch_ks_gemm(P, P.iks_t, 1024, 1025, lv1, *KG, out, B, s, used);
     if (O.ks_form != 1 && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s, O, used))
         return hipGetLastError();
     // items per block: TFHE_OPT_KS_SEL_ITEMS in {8, 16, 32} (default 8)

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "b9b3cb35de6e928c"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "1ad45ef93f0c22b2"; }
