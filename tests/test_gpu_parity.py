@@ -92,7 +92,7 @@ def test_key_switch_vs_oracle(oracle, pname, B, form):
     with c.options(ks_form={"sel": 1, "gemm": 2}.get(form, 0), ks_narrow=int(form.endswith("narrow"))):
         assert np.array_equal(c.key_switch(lv1), want)
         if form == "gemm":
-            assert ("k_key_switch_gemm<" in c.last_kernels()) == (pname != "uint4")
+            assert "k_key_switch_gemm<" in c.last_kernels()
 
 
 @pytest.mark.parametrize("B", [1024, 1500])
@@ -105,7 +105,7 @@ def test_key_switch_gemm_full_batches(oracle, B):
     lanes = c.key_switch(lv1)
     with c.options(ks_form=2):
         got = c.key_switch(lv1)
-        assert "k_key_switch_gemm<9>" in c.last_kernels()
+        assert "k_key_switch_gemm<9,2>" in c.last_kernels()
     assert np.array_equal(got, lanes)
     for i in (0, 511, 512, B - 1):
         assert np.array_equal(got[i], oracle.identity_key_switch(k.p, lv1[i], k.ck.ksk))
@@ -355,6 +355,23 @@ def test_lut_uint4_dispatch_plans(oracle, extra, form):
     assert np.array_equal(out[idx], want)
 
 
+def test_lut_uint4_gemm_key_switch(oracle):
+    """UINT4 key switch as the one-hot GEMM (basebit 5: one MFMA K-step per
+    coefficient and level, TFHE_OPT_KS_FORM = 2) on 1,300 LUT bootstraps:
+    bit-identical to the ring form (the default) and decrypting to f(m)."""
+    c, k = ctx_for(oracle, "uint4")
+    tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (5 * x + 2) % 16)
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    msgs = rng(1300).integers(0, 16, 1300).astype(np.uint32)
+    cts = sk.encrypt_lwe_message(msgs, 16, seed0=13000)
+    ring = c.bootstrap_lut_batch(cts, tv)
+    with c.options(ks_form=2):
+        got = c.bootstrap_lut_batch(cts, tv)
+        assert "k_key_switch_gemm<3,5>" in c.last_kernels()
+    assert np.array_equal(got, ring)
+    assert np.array_equal(sk.decrypt_lwe_message(got, 16), (5 * msgs + 2) % 16)
+
+
 def test_lut_uint4_golden_fixture(oracle):
     """The committed config-5 fixture (tests/golden/lut_uint4.npz) through
     tfhe_gpu_bootstrap_lut_batch with the oracle's seeded UINT4 key: bit-identical."""
@@ -540,7 +557,7 @@ def test_options_validation_and_report(oracle):
     g = rng(91)
     cts = u32rand(g, 3, k.p.n + 1)
     c.bootstrap_batch(cts)
-    gemm = "k_key_switch_gemm<9> + k_ks_gemm_reduce"
+    gemm = "k_key_switch_gemm<9,2> + k_ks_gemm_reduce"
     assert c.last_kernels() == "k_blind_rotate_wide<3,true,true> (latency form, fused) + " + gemm
     with c.options(arith=tfhe_amd.ARITH_REFERENCE):
         c.bootstrap_batch(cts)

@@ -201,7 +201,7 @@ def test_gpu_reencrypt_gemm_and_lanes_agree(oracle, P, keys, reenc_ab):
     hr = tfhe_amd.HipReencryptor(ctx, tfhe_amd.ProxyReencryptionKey(reenc_ab, P.basebit, P.iks_t))
     x = _random_cts(P, 1500, 1500)
     g = hr.reencrypt(x)
-    assert "k_key_switch_gemm<9>" in ctx.last_kernels()
+    assert "k_key_switch_gemm<9,2>" in ctx.last_kernels()
     with ctx.options(ks_form=0):
         lanes = hr.reencrypt(x)
         assert "k_key_switch_lanes<" in ctx.last_kernels()

@@ -247,17 +247,18 @@ enum RunKind : int {
 // sums.  G stays empty for the other forms (launch_key_switch ignores it).
 int ks_gemm_args(tfhe_gpu_ctx *c, size_t B, KsGemm &G) {
     G = KsGemm();
-    if ((c->opts.ks_form != 2 && (c->opts.ks_form != 3 || B < KS_GEMM_MIN_ITEMS)) || !ks_gemm_supported(c->K))
-        return TFHE_OK;
+    const bool want = c->opts.ks_form == 2 ||
+                      (c->opts.ks_form == 3 && B >= KS_GEMM_MIN_ITEMS && ks_gemm_auto(c->K.iks_t, c->K.basebit));
+    if (!want || !ks_gemm_supported(c->K)) return TFHE_OK;
     if (!c->d_ksk_gemm) {
-        hipError_t e = hipMalloc((void **)&c->d_ksk_gemm, ks_gemm_bytes(c->K, 1024, c->K.iks_t));
+        hipError_t e = hipMalloc((void **)&c->d_ksk_gemm, ks_gemm_bytes(c->K, 1024, c->K.iks_t, c->K.basebit));
         if (e != hipSuccess) return fail(c, TFHE_ERR_OOM, "hipMalloc(ksk gemm layout)");
     }
     if (!c->ksk_gemm_ok) {
-        HIPCHK(c, launch_ksk_to_gemm(c->K, c->d_ksk, c->d_ksk_gemm, 1024, c->K.iks_t, c->stream));
+        HIPCHK(c, launch_ksk_to_gemm(c->K, c->d_ksk, c->d_ksk_gemm, 1024, c->K.iks_t, c->K.basebit, c->stream));
         c->ksk_gemm_ok = true;
     }
-    int rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B, 1024));
+    int rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B, 1024, c->K.basebit));
     if (rc) return rc;
     G.kg = c->d_ksk_gemm;
     G.part = (uint32_t *)c->s_kspart.p;
@@ -1083,8 +1084,8 @@ static int reenc_key_load_one(tfhe_gpu_ctx *c, const uint32_t *key_encryptions, 
                              hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_key_zero_k0(c->K, k->d_key, (int)n, (int)t, (int)basebit, c->stream);
     if (e == hipSuccess && ks_gemm_supported((int)t, (int)basebit)) {  // §4.4b layout for the gemm form
-        e = hipMalloc((void **)&k->d_key_gemm, ks_gemm_bytes(c->K, (int)n, (int)t));
-        if (e == hipSuccess) e = launch_ksk_to_gemm(c->K, k->d_key, k->d_key_gemm, (int)n, (int)t, c->stream);
+        e = hipMalloc((void **)&k->d_key_gemm, ks_gemm_bytes(c->K, (int)n, (int)t, (int)basebit));
+        if (e == hipSuccess) e = launch_ksk_to_gemm(c->K, k->d_key, k->d_key_gemm, (int)n, (int)t, (int)basebit, c->stream);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
@@ -1119,7 +1120,7 @@ static int reencrypt_batch_one(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, con
     if (rc) return rc;
     KsGemm G;
     if (k->d_key_gemm) {
-        rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B, (int)c->P.n));
+        rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B, (int)c->P.n, (int)k->basebit));
         if (rc) return rc;
         G.kg = k->d_key_gemm;
         G.part = (uint32_t *)c->s_kspart.p;

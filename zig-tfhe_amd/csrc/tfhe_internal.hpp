@@ -108,14 +108,16 @@ struct KsGemm {
     uint32_t *part = nullptr;
 };
 // n_in: input coefficients (1024 for the identity key switch, n for a proxy
-// re-encryption key); t levels of basebit 2
-size_t ks_gemm_bytes(const KParams &P, int n_in, int t);
-size_t ks_gemm_part_bytes(const KParams &P, size_t B, int n_in);
+// re-encryption key); t levels of basebit 2 (t 7..9) or 5 (t 2, 3)
+size_t ks_gemm_bytes(const KParams &P, int n_in, int t, int basebit);
+size_t ks_gemm_part_bytes(const KParams &P, size_t B, int n_in, int basebit);
 bool ks_gemm_supported(const KParams &P);
 bool ks_gemm_supported(int t, int basebit);
+bool ks_gemm_auto(int t, int basebit);
 extern size_t KS_GEMM_MIN_ITEMS;
 constexpr size_t KS_GEMM_INPUT_SLACK = 16;  // bytes past the last input row the gemm form may read
-hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, int n_in, int t, hipStream_t s);
+hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, int n_in, int t, int basebit,
+                              hipStream_t s);
 hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32_t *ksk,
                              uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O = LaunchOpts(),
                              const char **used = nullptr, const KsGemm *G = nullptr);

@@ -2220,109 +2220,124 @@ constexpr int KG_ITEMS = 64 * KG_WAVES;  // items per workgroup
 typedef int kg_v4i __attribute__((ext_vector_type(4)));
 typedef int kg_v16i __attribute__((ext_vector_type(16)));
 
-// MFMA-layout KSK, built from the device KSK (k = 0 rows zeroed):
-// kg[j][ib][wt][b][lane][e] int8, lane = 32h + c: byte b of
-// KSK[i = 8ib + 4h + (e >> 2)][j][k = e & 3][w = 32wt + c] − 128 (w > n: 0 − 128).
-// n_in input coefficients (N for the identity key switch, n for the proxy
-// re-encryption key) in blocks of 8: coefficients past n_in select zero rows.
-__host__ __device__ __forceinline__ int kg_blocks(int n_in) { return (n_in + 7) / 8; }
-size_t ks_gemm_bytes(const KParams &P, int n_in, int t) {
+// MFMA-layout key, built from the device KSK (k = 0 rows zeroed), in blocks
+// of CB coefficients (kg_cb): kg[j][ib][wt][s][b][lane][e] int8, lane = 32h + c,
+// s < KS = kg_ksteps the MFMA K-steps of one level of one block:
+//   basebit 2: CB = 8, KS = 1, coefficient i = 8ib + 4h + (e >> 2), k = e & 3;
+//   basebit 5: CB = 4, KS = 4, coefficient i = 4ib + s, k = 16h + e;
+// byte b of KSK[i][j][k][w = 32wt + c] − 128 (w > n or i >= n_in: 0 − 128).
+__host__ __device__ __forceinline__ int kg_cb(int basebit) { return basebit == 2 ? 8 : 4; }
+__host__ __device__ __forceinline__ int kg_ksteps(int basebit) { return basebit == 2 ? 1 : 4; }
+__host__ __device__ __forceinline__ int kg_blocks(int n_in, int basebit) { return (n_in + kg_cb(basebit) - 1) / kg_cb(basebit); }
+size_t ks_gemm_bytes(const KParams &P, int n_in, int t, int basebit) {
     const size_t w32 = (size_t)(P.n + 1 + 31) / 32;
-    return (size_t)t * kg_blocks(n_in) * w32 * 4 * 1024;
+    return (size_t)t * kg_blocks(n_in, basebit) * w32 * kg_ksteps(basebit) * 4 * 1024;
 }
 __global__ void k_ksk_to_gemm(KParams P, const uint32_t *__restrict__ ksk, uint32_t *__restrict__ kg, size_t words,
-                              int n_in, int t) {
+                              int n_in, int t, int basebit) {
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // one u32 = bytes e = 4q .. 4q+3
     if (x >= words) return;
-    const int w32 = (P.n + 1 + 31) / 32, nib = kg_blocks(n_in);
+    const int w32 = (P.n + 1 + 31) / 32, nib = kg_blocks(n_in, basebit), ks = kg_ksteps(basebit);
+    const int base = 1 << basebit;
     const int q = (int)(x & 3), lane = (int)((x >> 2) & 63), b = (int)((x >> 8) & 3);
     size_t r = x >> 10;
+    const int st = (int)(r % ks);
+    r /= ks;
     const int wt = (int)(r % w32);
     r /= w32;
     const int ib = (int)(r % nib), j = (int)(r / nib);
-    const int h = lane >> 5, c = lane & 31;
-    const int i = 8 * ib + 4 * h + q, w = 32 * wt + c;
+    const int h = lane >> 5, c = lane & 31, w = 32 * wt + c;
     const size_t rs = (size_t)P.ks_stride;
     uint32_t v = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t word = (w <= P.n && i < n_in) ? ksk[((size_t)(4 * t) * i + 4 * j + k) * rs + w] : 0u;
-        v |= (((word >> (8 * b)) & 255u) ^ 128u) << (8 * k);  // byte − 128 as int8
+    for (int e4 = 0; e4 < 4; e4++) {
+        const int e = 4 * q + e4;
+        const int i = basebit == 2 ? 8 * ib + 4 * h + (e >> 2) : 4 * ib + st;
+        const int k = basebit == 2 ? (e & 3) : 16 * h + e;
+        const uint32_t word =
+            (w <= P.n && i < n_in) ? ksk[((size_t)(base * t) * i + (size_t)base * j + k) * rs + w] : 0u;
+        v |= (((word >> (8 * b)) & 255u) ^ 128u) << (8 * e4);  // byte − 128 as int8
     }
     kg[x] = v;
 }
 
-// s_waitcnt vmcnt(N) for the ring's two wave kinds (an immediate per case).
+// s_waitcnt vmcnt(N) (an immediate per case)
 template <int N>
 DEV void kg_wait() {
-    static_assert(N == 0 || N == 2 || (N >= 9 && N <= 11), "kg_wait");
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+    static_assert(N >= 0 && N <= 15, "kg_wait");
+#define KG_W(n_) if constexpr (N == n_) asm volatile("s_waitcnt vmcnt(" #n_ ")" ::: "memory");
+    KG_W(0) KG_W(1) KG_W(2) KG_W(3) KG_W(4) KG_W(5) KG_W(6) KG_W(7)
+    KG_W(8) KG_W(9) KG_W(10) KG_W(11) KG_W(12) KG_W(13) KG_W(14) KG_W(15)
+#undef KG_W
 }
 
-template <int T>
+template <int T, int BASEBIT>
 __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P, const uint32_t *__restrict__ lv1,
                                                                    const uint32_t *__restrict__ kg,
                                                                    uint32_t *__restrict__ part, size_t B,
                                                                    int ib_per_split, int n_in, int in_stride) {
-    constexpr int STEP_BYTES = 4 * 1024;                 // one level's 4 planes of one 32-word tile
-    constexpr int WORDS_BYTES = 8 * KG_ITEMS * 4;        // the block's 8 input words of the 512 items
+    constexpr int CB = BASEBIT == 2 ? 8 : 4;             // coefficients per block
+    constexpr int KS = BASEBIT == 2 ? 1 : 4;             // MFMA K-steps per level per block
+    constexpr int STEP_BYTES = KS * 4 * 1024;            // one level's K-steps x 4 planes of one 32-word tile
+    constexpr int WORDS_BYTES = CB * KG_ITEMS * 4;       // the block's CB input words of the 512 items
+    constexpr int WORD_DMAS = CB / 4;                    // 16-B pieces per item per block
     constexpr int BUF_BYTES = T * STEP_BYTES + WORDS_BYTES;
-    constexpr int STAGES = 3;                            // blocks ib (read), ib + 1 (landing), ib + 2 (issued)
+    constexpr int STAGES = 3 * BUF_BYTES <= 160 * 1024 ? 3 : 2;  // blocks read, landing (, issued)
+    constexpr int LOADER_DMAS = T * KS + WORD_DMAS;      // per block: waves 0-3 (KSK pieces + words) ...
+    constexpr int OTHER_DMAS = WORD_DMAS;                // ... and waves 4-7 (words)
     static_assert(STAGES * BUF_BYTES <= 160 * 1024, "gemm key-switch LDS");
     __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * BUF_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int v = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool loader = v < 4;  // waves 0-3 also issue the KSK pieces: 4 KB per level, 256 threads x 16 B
+    const bool loader = v < 4;  // waves 0-3 also issue the KSK pieces: 4 KB per instruction, 256 threads x 16 B
     const int w32 = (P.n + 1 + 31) / 32;
     const int wt = blockIdx.x;
-    const int nib = kg_blocks(n_in);
+    const int nib = kg_blocks(n_in, BASEBIT);
     const int ib_lo = blockIdx.z * ib_per_split, ib_hi = min(nib, ib_lo + ib_per_split);
     const size_t m_wg = (size_t)blockIdx.y * KG_ITEMS;
     const int h = lane >> 5, c = lane & 31;
-    // the block's 8 input words of item 256r + tid/2, half tid & 1 (16 B), r = 0, 1
-    const uint32_t *a_src[2];
+    // the block's input words: piece r of item (CB = 8) 256r + tid/2, half tid & 1, or (CB = 4) tid
+    const uint32_t *a_src[WORD_DMAS];
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const size_t m = m_wg + 256 * r + (tid >> 1);
-        a_src[r] = lv1 + (m < B ? m : B - 1) * (size_t)in_stride;
+    for (int r = 0; r < WORD_DMAS; r++) {
+        const size_t m = m_wg + (CB == 8 ? 256 * r + (tid >> 1) : tid);
+        a_src[r] = lv1 + (m < B ? m : B - 1) * (size_t)in_stride + (CB == 8 ? 4 * (tid & 1) : 0);
     }
     const uint32_t lds0 = (uint32_t)(size_t)(lds_void_t *)smem;
     // In flight per wave, oldest first: block ib's pieces, then block ib + 1's
-    // (loader waves T + 2 per block, the others 2), all by LDS-DMA: no VGPR
-    // holds a load in flight, so the only waits are the kg_wait below.
+    // (LOADER_DMAS or OTHER_DMAS per block), all by LDS-DMA: no VGPR holds a
+    // load in flight, so the only waits are the kg_wait below.
     auto issue = [&](int ib, int slot) {
         const uint32_t base = lds0 + slot * BUF_BYTES;
         if (loader) {
 #pragma unroll
-            for (int j = 0; j < T; j++) {
-                // block (j, ib, wt) is 4 KB = 1,024 words; thread tid's 16 B at word 4 tid
-                const uint32_t *src = kg + (((size_t)j * nib + ib) * w32 + wt) * 1024 + tid * 4;
-                const uint32_t dst = __builtin_amdgcn_readfirstlane(base + j * STEP_BYTES + (tid & ~63) * 16);
-                uint32_t keep;
-                asm volatile(
-                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                    : "=&s"(keep)
-                    : "v"(src), "s"(dst)
-                    : "memory");
-            }
-        }
-        // words [item][8]: 16 B per lane, item 256r + tid/2.  Coefficients past
-        // n_in select zero rows, so what a block's last words read there (the next
-        // row, or the caller's slack past the last one: launch_ks_gemm) is unused.
-        const int off_ok = 8 * ib + 4 * (tid & 1);
+            for (int j = 0; j < T; j++)
 #pragma unroll
-        for (int r = 0; r < 2; r++) {
+                for (int st = 0; st < KS; st++) {
+                    // block (j, ib, wt) is KS x 4 KB; thread tid's 16 B of K-step st at word 1,024 st + 4 tid
+                    const uint32_t *src = kg + ((((size_t)j * nib + ib) * w32 + wt) * KS + st) * 1024 + tid * 4;
+                    const uint32_t dst =
+                        __builtin_amdgcn_readfirstlane(base + j * STEP_BYTES + st * 4096 + (tid & ~63) * 16);
+                    uint32_t keep;
+                    asm volatile(
+                        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                        : "=&s"(keep)
+                        : "v"(src), "s"(dst)
+                        : "memory");
+                }
+        }
+        // words [item][CB], 16 B per lane.  Coefficients past n_in select zero
+        // rows, so what a block's last words read there (the next row, or the
+        // caller's slack past the last one: launch_ks_gemm) is unused.
+#pragma unroll
+        for (int r = 0; r < WORD_DMAS; r++) {
             const uint32_t dst =
                 __builtin_amdgcn_readfirstlane(base + T * STEP_BYTES + r * 256 * 32 + (tid & ~63) * 16);
             uint32_t keep;
             asm volatile(
                 "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                 : "=&s"(keep)
-                : "v"(a_src[r] + off_ok), "s"(dst)
+                : "v"(a_src[r] + CB * ib), "s"(dst)
                 : "memory");
         }
     };
@@ -2331,42 +2346,78 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
     for (int s = 0; s < 2; s++)
 #pragma unroll
         for (int b = 0; b < 4; b++) acc[s][b] = kg_v16i{};
-    const uint32_t prec = 1u << (32 - (1 + 2 * T));
-    if (ib_lo < ib_hi) issue(ib_lo, 0);
-    if (ib_lo + 1 < ib_hi) issue(ib_lo + 1, 1);
+    const uint32_t prec = 1u << (32 - (1 + BASEBIT * T));
+#pragma unroll
+    for (int k = 0; k < STAGES - 1; k++)
+        if (ib_lo + k < ib_hi) issue(ib_lo + k, k);
     for (int ib = ib_lo; ib < ib_hi; ib++) {
         const int slot = (ib - ib_lo) % STAGES;
-        if (ib + 1 < ib_hi) {  // block ib + 1 may stay in flight
-            if (loader) kg_wait<T + 2>();
-            else kg_wait<2>();
+        // blocks ib + 1 .. ib + STAGES - 2 may stay in flight
+        const int ahead = min(STAGES - 2, ib_hi - 1 - ib);
+        if (ahead == 1) {
+            if (loader) kg_wait<LOADER_DMAS>();
+            else kg_wait<OTHER_DMAS>();
         } else {
             kg_wait<0>();
         }
         __syncthreads();  // block ib landed for every wave; every wave done with block ib - 1
-        if (ib + 2 < ib_hi) issue(ib + 2, (slot + 2) % STAGES);  // into block ib - 1's slot
+        if (ib + STAGES - 1 < ib_hi) issue(ib + STAGES - 1, (slot + STAGES - 1) % STAGES);  // block ib - 1's slot
         const unsigned char *buf = smem + slot * BUF_BYTES;
         const uint32_t *words = reinterpret_cast<const uint32_t *>(buf + T * STEP_BYTES);
-        uint32_t pk[2][4];
+        if constexpr (BASEBIT == 2) {
+            uint32_t pk[2][4];
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const kg_v4i wv = *reinterpret_cast<const kg_v4i *>(words + (64 * v + 32 * s + c) * 8 + 4 * h);
+            for (int s = 0; s < 2; s++) {
+                const kg_v4i wv = *reinterpret_cast<const kg_v4i *>(words + (64 * v + 32 * s + c) * 8 + 4 * h);
 #pragma unroll
-            for (int q = 0; q < 4; q++) pk[s][q] = ((uint32_t)wv[q] + prec) >> (32 - 2 * T);
-        }
-#pragma unroll
-        for (int j = 0; j < T; j++) {
-            kg_v4i a[2];
-#pragma unroll
-            for (int s = 0; s < 2; s++)
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    a[s][q] = (int)(1u << (8u * ((pk[s][q] >> (2 * (T - 1 - j))) & 3u)));
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const kg_v4i bf = *reinterpret_cast<const kg_v4i *>(buf + j * STEP_BYTES + b * 1024 + lane * 16);
-#pragma unroll
-                for (int s = 0; s < 2; s++) acc[s][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bf, acc[s][b], 0, 0, 0);
+                for (int q = 0; q < 4; q++) pk[s][q] = ((uint32_t)wv[q] + prec) >> (32 - 2 * T);
             }
+#pragma unroll
+            for (int j = 0; j < T; j++) {
+                kg_v4i a[2];
+#pragma unroll
+                for (int s = 0; s < 2; s++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        a[s][q] = (int)(1u << (8u * ((pk[s][q] >> (2 * (T - 1 - j))) & 3u)));
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const kg_v4i bf = *reinterpret_cast<const kg_v4i *>(buf + j * STEP_BYTES + b * 1024 + lane * 16);
+#pragma unroll
+                    for (int s = 0; s < 2; s++)
+                        acc[s][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bf, acc[s][b], 0, 0, 0);
+                }
+            }
+        } else {  // basebit 5: one K-step per (coefficient, level), lane half h holds k = 16h .. 16h+15
+            uint32_t pk[2][4];
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const kg_v4i wv = *reinterpret_cast<const kg_v4i *>(words + (64 * v + 32 * s + c) * 4);
+#pragma unroll
+                for (int q = 0; q < 4; q++) pk[s][q] = ((uint32_t)wv[q] + prec) >> (32 - BASEBIT * T);
+            }
+#pragma unroll
+            for (int j = 0; j < T; j++)
+#pragma unroll
+                for (int st = 0; st < KS; st++) {
+                    kg_v4i a[2];
+#pragma unroll
+                    for (int s = 0; s < 2; s++) {
+                        const uint32_t d = (pk[s][st] >> (BASEBIT * (T - 1 - j))) & 31u;
+                        const uint32_t one = 1u << (8u * (d & 3u));
+                        const int word = (int)(d >> 2) - 4 * h;  // 0..3 when k = d sits in this lane half
+#pragma unroll
+                        for (int q = 0; q < 4; q++) a[s][q] = word == q ? (int)one : 0;
+                    }
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const kg_v4i bf = *reinterpret_cast<const kg_v4i *>(buf + j * STEP_BYTES + st * 4096 +
+                                                                            b * 1024 + lane * 16);
+#pragma unroll
+                        for (int s = 0; s < 2; s++)
+                            acc[s][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bf, acc[s][b], 0, 0, 0);
+                    }
+                }
         }
     }
     // partial sums of this K split: part[z][m][w], w < n + 1
@@ -2385,15 +2436,16 @@ __global__ __launch_bounds__(64 * KG_WAVES, 1) void k_key_switch_gemm(KParams P,
         }
 }
 
-// out[m][w] = [w = n]·b_m − Σ_z part[z][m][w] − 8·blocks·t·128·0x01010101 (mod 2^32)
+// out[m][w] = [w = n]·b_m − Σ_z part[z][m][w] − CB·blocks·t·128·0x01010101 (mod 2^32)
 __global__ void k_ks_gemm_reduce(KParams P, const uint32_t *__restrict__ lv1, const uint32_t *__restrict__ part,
-                                 uint32_t *__restrict__ out, size_t B, int splits, int n_in, int in_stride, int t) {
+                                 uint32_t *__restrict__ out, size_t B, int splits, int n_in, int in_stride, int t,
+                                 int basebit) {
     const int n1 = P.n + 1;
     const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= B * n1) return;
     const size_t m = x / n1;
     const int w = (int)(x % n1);
-    uint32_t r = (uint32_t)(8 * kg_blocks(n_in) * t) * 128u * 0x01010101u;
+    uint32_t r = (uint32_t)(kg_cb(basebit) * kg_blocks(n_in, basebit) * t) * 128u * 0x01010101u;
     for (int z = 0; z < splits; z++) r += part[(size_t)z * B * n1 + x];
     out[x] = (w == P.n ? lv1[m * (size_t)in_stride + n_in] : 0u) - r;
 }
@@ -3204,15 +3256,16 @@ static bool launch_ks_lanes(const KParams &P, int t_, int basebit, const uint32_
     return true;
 }
 
-static hipError_t launch_ks_gemm(const KParams &P, int t, int n_in, int in_stride, const uint32_t *in,
+static hipError_t launch_ks_gemm(const KParams &P, int t, int basebit, int n_in, int in_stride, const uint32_t *in,
                                  const KsGemm &G, uint32_t *out, size_t B, hipStream_t s, const char **used);
 
 hipError_t launch_reencrypt(const KParams &P, int t_, int basebit, const uint32_t *in, const uint32_t *key,
                             uint32_t *out, size_t B, hipStream_t s, const LaunchOpts &O, const char **used,
                             const KsGemm *KG) {
     if (B == 0) return hipSuccess;
-    if (KG && KG->kg && KG->part && ks_gemm_supported(t_, basebit) && (O.ks_form == 2 || O.ks_form == 3))
-        return launch_ks_gemm(P, t_, P.n, P.n + 1, in, *KG, out, B, s, used);
+    if (KG && KG->kg && KG->part && ks_gemm_supported(t_, basebit) &&
+        (O.ks_form == 2 || (O.ks_form == 3 && ks_gemm_auto(t_, basebit))))
+        return launch_ks_gemm(P, t_, basebit, P.n, P.n + 1, in, *KG, out, B, s, used);
     if (!launch_ks_lanes(P, t_, basebit, in, P.n, P.n + 1, key, out, B, s, O, used)) return hipErrorInvalidValue;
     return hipGetLastError();
 }
@@ -3223,53 +3276,64 @@ bool reencrypt_supported(int t_, int basebit) {
 }
 
 // K splits of the gemm form: enough workgroups for one per CU.
-static int ks_gemm_splits(const KParams &P, size_t B, int n_in) {
+static int ks_gemm_splits(const KParams &P, size_t B, int n_in, int basebit) {
     const size_t tiles = (size_t)(P.n + 1 + 31) / 32 * ((B + KG_ITEMS - 1) / KG_ITEMS);
     const size_t z = std::max<size_t>(1, device_cus() / tiles);
-    return (int)std::min<size_t>(z, (size_t)kg_blocks(n_in));
+    return (int)std::min<size_t>(z, (size_t)kg_blocks(n_in, basebit));
 }
-size_t ks_gemm_part_bytes(const KParams &P, size_t B, int n_in) {
-    return (size_t)ks_gemm_splits(P, B, n_in) * B * (P.n + 1) * 4;
+size_t ks_gemm_part_bytes(const KParams &P, size_t B, int n_in, int basebit) {
+    return (size_t)ks_gemm_splits(P, B, n_in, basebit) * B * (P.n + 1) * 4;
 }
 
 // One-hot GEMM key switch of B inputs of in_stride words (n_in coefficients, then b)
-// against a MFMA-layout key of t levels (ks_gemm_supported).  The kernel reads
-// whole blocks of 8 coefficients: when 8·ceil(n_in/8) > in_stride, the input
-// buffer needs 16 readable bytes past its last row (KS_GEMM_INPUT_SLACK).
-static hipError_t launch_ks_gemm(const KParams &P, int t, int n_in, int in_stride, const uint32_t *in,
+// against a MFMA-layout key of t levels of basebit (ks_gemm_supported).  The
+// kernel reads whole blocks of coefficients: when they reach past in_stride the
+// input buffer needs KS_GEMM_INPUT_SLACK readable bytes past its last row.
+static hipError_t launch_ks_gemm(const KParams &P, int t, int basebit, int n_in, int in_stride, const uint32_t *in,
                                  const KsGemm &G, uint32_t *out, size_t B, hipStream_t s, const char **used) {
-    const int nib = kg_blocks(n_in);
-    const int z = ks_gemm_splits(P, B, n_in);
+    const int nib = kg_blocks(n_in, basebit);
+    const int z = ks_gemm_splits(P, B, n_in, basebit);
     const int per = (nib + z - 1) / z;
     const int splits = (nib + per - 1) / per;
     dim3 grid((unsigned)((P.n + 1 + 31) / 32), (unsigned)((B + KG_ITEMS - 1) / KG_ITEMS), (unsigned)splits),
         block(64 * KG_WAVES);
-    switch (t) {
-    case 7: hipLaunchKernelGGL((k_key_switch_gemm<7>), grid, block, 0, s, P, in, G.kg, G.part, B, per, n_in, in_stride); break;
-    case 8: hipLaunchKernelGGL((k_key_switch_gemm<8>), grid, block, 0, s, P, in, G.kg, G.part, B, per, n_in, in_stride); break;
-    case 9: hipLaunchKernelGGL((k_key_switch_gemm<9>), grid, block, 0, s, P, in, G.kg, G.part, B, per, n_in, in_stride); break;
-    default: return hipErrorInvalidValue;
-    }
+#define KG_LAUNCH(T_, BB_)                                                                                       \
+    do {                                                                                                         \
+        hipLaunchKernelGGL((k_key_switch_gemm<T_, BB_>), grid, block, 0, s, P, in, G.kg, G.part, B, per, n_in, \
+                           in_stride);                                                                           \
+        if (used) *used = "k_key_switch_gemm<" #T_ "," #BB_ "> + k_ks_gemm_reduce";                              \
+    } while (0)
+    if (basebit == 2 && t == 9) KG_LAUNCH(9, 2);
+    else if (basebit == 2 && t == 8) KG_LAUNCH(8, 2);
+    else if (basebit == 2 && t == 7) KG_LAUNCH(7, 2);
+    else if (basebit == 5 && t == 3) KG_LAUNCH(3, 5);
+    else if (basebit == 5 && t == 2) KG_LAUNCH(2, 5);
+    else return hipErrorInvalidValue;
+#undef KG_LAUNCH
     const size_t total = B * (size_t)(P.n + 1);
     hipLaunchKernelGGL(k_ks_gemm_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, P, in, G.part, out, B,
-                       splits, n_in, in_stride, t);
-    if (used) *used = t == 9 ? "k_key_switch_gemm<9> + k_ks_gemm_reduce"
-                      : t == 8 ? "k_key_switch_gemm<8> + k_ks_gemm_reduce"
-                               : "k_key_switch_gemm<7> + k_ks_gemm_reduce";
+                       splits, n_in, in_stride, t, basebit);
     return hipGetLastError();
 }
 
-bool ks_gemm_supported(int t, int basebit) { return basebit == 2 && t >= 7 && t <= 9; }
+bool ks_gemm_supported(int t, int basebit) {
+    return (basebit == 2 && t >= 7 && t <= 9) || (basebit == 5 && (t == 2 || t == 3));
+}
 bool ks_gemm_supported(const KParams &P) { return ks_gemm_supported(P.iks_t, P.basebit); }
 // Batches from this size take the GEMM under TFHE_OPT_KS_FORM = 3: it is the
 // faster form from 64 items up (0.050 vs 0.218 ms at 64, 0.090 vs 0.239 ms at
 // 1,024, 0.35 vs 0.94 ms at 4,096; profiles/r03k_ks_gemm.txt), and a batch of
 // one still fills 242 workgroups (22 tiles x 11 K splits).
 size_t KS_GEMM_MIN_ITEMS = 1;
+// TFHE_OPT_KS_FORM = 3 takes the GEMM for these parameter sets (basebit 5 only
+// when forced, until it is measured against the ring form)
+bool ks_gemm_auto(int t, int basebit) { return basebit == 2 && ks_gemm_supported(t, basebit); }
 
-hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, int n_in, int t, hipStream_t s) {
-    const size_t words = ks_gemm_bytes(P, n_in, t) / 4;
-    hipLaunchKernelGGL(k_ksk_to_gemm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, ksk, kg, words, n_in, t);
+hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, int n_in, int t, int basebit,
+                              hipStream_t s) {
+    const size_t words = ks_gemm_bytes(P, n_in, t, basebit) / 4;
+    hipLaunchKernelGGL(k_ksk_to_gemm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, ksk, kg, words, n_in,
+                       t, basebit);
     return hipGetLastError();
 }
 
@@ -3280,8 +3344,8 @@ hipError_t launch_key_switch(const KParams &P, const uint32_t *lv1, const uint32
     // basebit 2 from KS_GEMM_MIN_ITEMS items, else lanes; 2 the GEMM wherever it
     // applies; 0 lanes; 1 the select / gather forms
     const bool gemm_ok = KG && KG->kg && KG->part && ks_gemm_supported(P);
-    if (gemm_ok && (O.ks_form == 2 || (O.ks_form == 3 && B >= KS_GEMM_MIN_ITEMS)))
-        return launch_ks_gemm(P, P.iks_t, 1024, 1025, lv1, *KG, out, B, s, used);
+    if (gemm_ok && (O.ks_form == 2 || (O.ks_form == 3 && B >= KS_GEMM_MIN_ITEMS && ks_gemm_auto(P.iks_t, P.basebit))))
+        return launch_ks_gemm(P, P.iks_t, P.basebit, 1024, 1025, lv1, *KG, out, B, s, used);
     if (O.ks_form != 1 && launch_ks_lanes(P, P.iks_t, P.basebit, lv1, 1024, 1025, ksk, out, B, s, O, used))
         return hipGetLastError();
     // items per block: TFHE_OPT_KS_SEL_ITEMS in {8, 16, 32} (default 8)

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "1ad45ef93f0c22b2"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "9b5b5487d60d1094"; }
