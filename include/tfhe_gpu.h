@@ -133,7 +133,7 @@ enum {
                                      5 octo (8 items per workgroup, two gate waves per SIMD) */
     TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
     TFHE_OPT_KS_FORM = 3,         /* key switch: 3 auto (default: the one-hot GEMM on the matrix
-                                     cores for basebit 2, else lanes), 0 lanes,
+                                     cores for basebit 2 and 5, else lanes), 0 lanes / ring,
                                      1 select / gather, 2 the GEMM at any batch (basebit 2; other
                                      parameter sets fall back to lanes) */
     TFHE_OPT_KS_NARROW = 4,       /* basebit 2: 0 auto (default), 1 32-word x 4-wave blocks */

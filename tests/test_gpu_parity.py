@@ -320,7 +320,7 @@ def test_lut_config5_full_4096_uint4(oracle):
     msgs = rng(4096).integers(0, m, 4096).astype(np.uint32)
     cts = sk.encrypt_lwe_message(msgs, m, seed0=40960)
     out = c.bootstrap_lut_batch(cts, tv)
-    assert "k_key_switch_ring<" in c.last_kernels()
+    assert "k_key_switch_gemm<3,5>" in c.last_kernels()
     assert np.array_equal(sk.decrypt_lwe_message(out, m), (msgs * msgs + 3) % m)
     idx = [0, 1, 255, 1023, 1024, 2047, 3071, 3840, 4000, 4095]
     want = oracle.gate_batch(k.p, np.full(len(idx), 255, np.uint8), cts[idx], cts[idx], k.ck, testvec=tv,
@@ -357,17 +357,18 @@ def test_lut_uint4_dispatch_plans(oracle, extra, form):
 
 def test_lut_uint4_gemm_key_switch(oracle):
     """UINT4 key switch as the one-hot GEMM (basebit 5: one MFMA K-step per
-    coefficient and level, TFHE_OPT_KS_FORM = 2) on 1,300 LUT bootstraps:
-    bit-identical to the ring form (the default) and decrypting to f(m)."""
+    coefficient and level; the default) on 1,300 LUT bootstraps: bit-identical
+    to the ring form (TFHE_OPT_KS_FORM = 0) and decrypting to f(m)."""
     c, k = ctx_for(oracle, "uint4")
     tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (5 * x + 2) % 16)
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
     msgs = rng(1300).integers(0, 16, 1300).astype(np.uint32)
     cts = sk.encrypt_lwe_message(msgs, 16, seed0=13000)
-    ring = c.bootstrap_lut_batch(cts, tv)
-    with c.options(ks_form=2):
-        got = c.bootstrap_lut_batch(cts, tv)
-        assert "k_key_switch_gemm<3,5>" in c.last_kernels()
+    with c.options(ks_form=0):
+        ring = c.bootstrap_lut_batch(cts, tv)
+        assert "k_key_switch_ring<" in c.last_kernels()
+    got = c.bootstrap_lut_batch(cts, tv)
+    assert "k_key_switch_gemm<3,5>" in c.last_kernels()
     assert np.array_equal(got, ring)
     assert np.array_equal(sk.decrypt_lwe_message(got, 16), (5 * msgs + 2) % 16)
 
@@ -441,16 +442,16 @@ def test_device_resident_api_with_torch(oracle):
 
 @pytest.mark.parametrize("gw", [0, 1, 2, 4, 8])
 def test_lut_uint4_key_switch_item_groups(oracle, gw):
-    """UINT4 key switch: the default ring form (gw 0: 4 item groups sharing one
-    4-deep ring per block) and the lane form with 1, 2, 4 or 8 item groups per block
-    (TFHE_OPT_KS_ITEM_GROUPS): 300 LUT bootstraps, samples past the first group
-    bit-exact vs the oracle."""
+    """UINT4 key switch under TFHE_OPT_KS_FORM = 0: the ring form (gw 0: 4 item
+    groups sharing one 4-deep ring per block) and the lane form with 1, 2, 4 or 8
+    item groups per block (TFHE_OPT_KS_ITEM_GROUPS): 300 LUT bootstraps, samples
+    past the first group bit-exact vs the oracle."""
     c, k = ctx_for(oracle, "uint4")
     tv = tfhe_amd.lut_generate(c.params, 16, lambda x: (3 * x + 5) % 16)
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
     msgs = rng(23).integers(0, 16, 300).astype(np.uint32)
     cts = sk.encrypt_lwe_message(msgs, 16, seed0=4242)
-    with c.options(ks_item_groups=gw):
+    with c.options(ks_item_groups=gw, ks_form=0):
         out = c.bootstrap_lut_batch(cts, tv)
         assert ("k_key_switch_ring<" in c.last_kernels()) == (gw == 0)
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (3 * msgs + 5) % 16)

@@ -3325,9 +3325,10 @@ bool ks_gemm_supported(const KParams &P) { return ks_gemm_supported(P.iks_t, P.b
 // 1,024, 0.35 vs 0.94 ms at 4,096; profiles/r03k_ks_gemm.txt), and a batch of
 // one still fills 242 workgroups (22 tiles x 11 K splits).
 size_t KS_GEMM_MIN_ITEMS = 1;
-// TFHE_OPT_KS_FORM = 3 takes the GEMM for these parameter sets (basebit 5 only
-// when forced, until it is measured against the ring form)
-bool ks_gemm_auto(int t, int basebit) { return basebit == 2 && ks_gemm_supported(t, basebit); }
+// TFHE_OPT_KS_FORM = 3 takes the GEMM wherever it applies: at basebit 5 too
+// (UINT4, 4,096 items: 0.90 ms against the ring form's 1.24 ms, config 5
+// 182.5 k -> 186.0 k/s; profiles/r03m_ks_gemm_uint4.txt)
+bool ks_gemm_auto(int t, int basebit) { return ks_gemm_supported(t, basebit); }
 
 hipError_t launch_ksk_to_gemm(const KParams &P, const uint32_t *ksk, uint32_t *kg, int n_in, int t, int basebit,
                               hipStream_t s) {

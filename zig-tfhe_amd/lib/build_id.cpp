@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "9b5b5487d60d1094"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "91c5540e9fe579c9"; }
