@@ -562,7 +562,7 @@ def main():
                        "global_batch": total, "params": args.params, "parallelism": f"dp{world}"},
             "roofline": roof,
             "roofline_hbm_accounting": hbm,
-            "key_switch": {"kernel": kernels.split(" + ")[-1], "avg_ms": round(ks_avg_s * 1e3, 3)},
+            "key_switch": {"kernel": " + ".join(kernels.split(" + ")[1:]), "avg_ms": round(ks_avg_s * 1e3, 3)},
             "margin_guard": {"recomputed_items": recomputed, "items": B * args.steps,
                              "note": "fused arithmetic; items that round a value 1/4 or more off its integer are "
                                      "redone in the reference's expression trees inside the timed launches "
