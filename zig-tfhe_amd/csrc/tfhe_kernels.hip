@@ -14,10 +14,12 @@
 //    `fp contract(off)` plus -ffp-contract=off);
 //  - fused (FU = true; the default at the L=3 / Bg=2^6 sets): explicit fused
 //    multiply-adds (fmad below, __builtin_fma) in the reference's operation
-//    order, with a margin guard on every rounding: an item whose fused values
-//    come within 1/8 of a tie is recomputed in the reference trees
+//    order, with a margin guard on every rounding: an item that rounds a fused
+//    value 1/4 or more off its integer is recomputed in the reference trees
 //    (torus_from_f64_guarded, launch_br_recompute), so both give the
 //    reference's integers.
+// The key switch (k_key_switch_gemm, the default form) is integer-exact: a
+// one-hot int8 GEMM on the matrix cores.
 // Twiddles are uploaded from the host (never sin/cos on the device).  Exact
 // power-of-two rescalings (×2 in ifft1024, ×0.5 in fmaInFd1024 and fft1024)
 // are folded, which leaves every result bit-identical.
