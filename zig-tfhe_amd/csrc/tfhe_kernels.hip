@@ -2002,13 +2002,15 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
             }
             __builtin_amdgcn_sched_barrier(0);
             C2 d[1][8];
+            const uint32_t msbs = digit_msbs(L, P.bgbit);  // flipped tmp words: one v_bfe_i32 per digit
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int m = br3(q);
                 const bool n0 = ((rb + 64 * m) & 1024) != 0, n1 = ((rb + 64 * (m + 8)) & 1024) != 0;
-                const uint32_t x0 = (n0 ? 0u - rot[m] : rot[m]) - own[m] + P.offset;
-                const uint32_t x1 = (n1 ? 0u - rot[m + 8] : rot[m + 8]) - own[m + 8] + P.offset;
-                d[0][q] = twist_in<FU>(digit_f64(x0, level, P.bgbit), digit_f64(x1, level, P.bgbit), twist_t[64 * m]);
+                const uint32_t x0 = ((n0 ? 0u - rot[m] : rot[m]) - own[m] + P.offset) ^ msbs;
+                const uint32_t x1 = ((n1 ? 0u - rot[m + 8] : rot[m + 8]) - own[m + 8] + P.offset) ^ msbs;
+                d[0][q] = twist_in<FU>(digit_f64_flipped(x0, level, P.bgbit), digit_f64_flipped(x1, level, P.bgbit),
+                                       twist_t[64 * m]);
             }
             fft512<1, false, FU>(d, s_prod[0][w], T, t);
             // this row's terms of fmaInFd1024 for both outputs, every frequency

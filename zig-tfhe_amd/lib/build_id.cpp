@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "91c5540e9fe579c9"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "5b1f3d172f15b25d"; }
