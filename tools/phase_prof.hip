@@ -41,7 +41,7 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int rep = 0; rep < 2; rep++) {
-        unsigned long long z[64] = {0};
+        unsigned long long z[128] = {0};
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
         CK(hipEventRecord(e0));
         LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
@@ -52,21 +52,23 @@ int main(int argc, char **argv) {
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-        unsigned long long c[64];
+        unsigned long long c[128];
         CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
         if (O.br_form == 3) {  // latency form: per wave, per phase (ticks per step per gate)
-            const char *wn[7] = {"digits+fwd+publish", "barrier1", "mac+prefetch", "barrier2", "inverse+add", "barrier3", "tail"};
+            const char *wn[16] = {"fwd(other)", "barrier1", "sum", "barrier2", "inverse(other)", "barrier3", "tail", "-",
+                                  "row: gather", "row: digits+twist", "row: fft", "row: terms", "inv: fft", "inv: untwist+add", "row: prefetch issue", "-"};
             printf("rep %d: %.3f ms (%zu gates); s_memtime ticks per step, per wave:\n", rep, ms, B);
-            for (int k = 0; k < 6; k++) {
+            for (int k = 0; k < 16; k++) {
+                if (k == 6 || k == 7 || k > 14) continue;
                 printf("  %-20s", wn[k]);
-                for (int w = 0; w < 8; w++) printf(" %8.1f", c[w * 8 + k] / (double)B / P.n);
+                for (int w = 0; w < 8; w++) printf(" %8.1f", c[w * 16 + k] / (double)B / P.n);
                 printf("\n");
             }
             continue;
         }
         const char *nm[8] = {"tmp", "fwd-fft(pairs)", "barrier1", "mac", "barrier2", "inverse+add", "tail", "dma-issue"};
         double tot = 0;
-        for (int k = 0; k < 8; k++) tot += c[k];
+        for (int k = 0; k < 8; k++) tot += c[k];  // whole form: [k], loaders [8 + q]
         printf("rep %d: %.3f ms; cycles per wave-step (s_memtime ticks):\n", rep, ms);
         for (int k = 0; k < 8; k++)
             printf("  %-16s %10.1f  %5.1f%%\n", nm[k], c[k] / (double)B / P.n, 100.0 * c[k] / tot);

@@ -50,10 +50,10 @@ struct PhaseProf {
 #ifdef TFHE_PHASE_PROF
     uint64_t last;
     int cur;
-    uint64_t acc[8];
+    uint64_t acc[16];
     DEV void start() {
         cur = 0;
-        for (int k = 0; k < 8; k++) acc[k] = 0;
+        for (int k = 0; k < 16; k++) acc[k] = 0;
         last = __builtin_amdgcn_s_memtime();
     }
     DEV void mark(int k) {
@@ -68,7 +68,7 @@ struct PhaseProf {
 #endif
 };
 #ifdef TFHE_PHASE_PROF
-__device__ unsigned long long g_phase_cycles[64];  // [wave][phase] for the wide form
+__device__ unsigned long long g_phase_cycles[128];  // [wave][phase < 16] for the wide form
 #endif
 
 DEV C2 c2(double x, double y) {
@@ -1927,6 +1927,20 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
 constexpr int BW_WAVES = 8;
 constexpr size_t BR_WIDE_MAX_ITEMS = 512;  // measured: 1 gate 4.3 vs 9.9 ms; 512 gates 8.8 vs 10.2 ms; 1024: 17.1 vs 10.4 ms
 
+// Row wave w's BK row of the coming step: parts a|b, every frequency t + 64q.
+DEV void wide_prefetch(double2 (*kr)[2], const double2 *__restrict__ nb, int w, int t) {
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+#pragma unroll
+        for (int h = 0; h < 2; h++) kr[q][h] = nb[((size_t)w * 8 + q) * 128 + h * 64 + t];
+}
+#ifndef WIDE_INV_W0  // A/B: 0 = the round-2 inverse waves 0, 1
+#define WIDE_INV_W0 2
+#endif
+#ifndef WIDE_PF_LATE_MASK  // A/B: 0 = every row wave prefetches right after its terms (round-2 schedule)
+#define WIDE_PF_LATE_MASK 0xff
+#endif
+
 template <int L, bool SMALL, bool FU = false>
 __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
@@ -1979,6 +1993,22 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     T.init(s_tw, TT);
     const C2 *twist_t = s_twist + t;
     __syncthreads();
+    // inverse waves: WIDE_INV_W0 and WIDE_INV_W0 + 1 transform polynomials 0 and 1.
+    // Waves 2 and 3 by default: their SIMDs carry one row wave, those of waves
+    // 0 and 1 two (rows 4, 5), and the other row waves' BK prefetch issues during
+    // the inverse phase on SIMDs the inverse does not use.
+    const int ipoly = w - WIDE_INV_W0;
+    const bool is_inv = ipoly == 0 || ipoly == 1;
+    // row waves that issue their BK prefetch in the inverse phase (the others
+    // right after their terms)
+    const bool pf_late = w < 2 * L && !is_inv && ((WIDE_PF_LATE_MASK >> w) & 1);
+    // the inverse waves keep their polynomial's 16 accumulator words per lane
+    // in registers: the update then waits for no LDS read
+    uint32_t accr[16];
+    if (is_inv) {
+#pragma unroll
+        for (int m = 0; m < 16; m++) accr[m] = s_acc[ipoly * 1024 + t + 64 * m];
+    }
 
     int at_next = s_at[0];  // a~ read one step ahead (its wait would drain every LDS op)
     uint32_t near = NEAR_NONE;  // FU: margin guard (the inverse waves)
@@ -1994,6 +2024,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
             const uint32_t *pa = s_acc + poly * 1024;
             // gathers and own words first, arithmetic after (one wait)
             uint32_t rot[16], own[16];
+            pp.mark(8);
             const int rb = (t - at) & 2047;
 #pragma unroll
             for (int m = 0; m < 16; m++) {
@@ -2001,6 +2032,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
                 own[m] = pa[t + 64 * m];
             }
             __builtin_amdgcn_sched_barrier(0);
+            pp.mark(9);
             C2 d[1][8];
             const uint32_t msbs = digit_msbs(L, P.bgbit);  // flipped tmp words: one v_bfe_i32 per digit
 #pragma unroll
@@ -2012,7 +2044,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
                 d[0][q] = twist_in<FU>(digit_f64_flipped(x0, level, P.bgbit), digit_f64_flipped(x1, level, P.bgbit),
                                        twist_t[64 * m]);
             }
+            pp.mark(10);
             fft512<1, false, FU>(d, s_prod[0][w], T, t);
+            pp.mark(11);
             // this row's terms of fmaInFd1024 for both outputs, every frequency
             // (after this wave's exchanges in s_prod[0][w])
 #pragma unroll
@@ -2020,13 +2054,18 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
                 s_prod[0][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][0]);
                 s_prod[1][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][1]);
             }
-            if (i + 1 < n) {  // next step's BK row, landing under the sum, inverse and forward phases
-                const double2 *nb = bkd + (size_t)(i + 1) * trgsw;
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-#pragma unroll
-                    for (int h = 0; h < 2; h++) kr[q][h] = nb[((size_t)w * 8 + q) * 128 + h * 64 + t];
-            }
+            pp.mark(14);
+#ifndef TFHE_KO_WIDE_PREFETCH
+            // next step's BK row, landing under the sum, inverse and forward
+            // phases.  The inverse waves (2, 3) issue it here; the other row
+            // waves wait for the inverse phase, where they are idle: 16 KB per
+            // wave through the CU's vector-memory path no longer queues behind
+            // 5 other waves' at the end of the forward phase, which is the
+            // critical path (rows 4 and 5 share SIMDs with rows 0 and 1):
+            // 104.7 -> 101.8 ms per 16-bit adder with the inverse on waves 2, 3
+            // (profiles/r03q_wide_prefetch_inverse.txt).
+            if (i + 1 < n && !pf_late) wide_prefetch(kr, bkd + (size_t)(i + 1) * trgsw, w, t);
+#endif
         }
         pp.mark(1);
         __syncthreads();  // every row's terms are in place
@@ -2046,18 +2085,28 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
         pp.mark(3);
         __syncthreads();  // both product spectra complete
         pp.mark(4);
-        if (w < 2) {
+#ifndef TFHE_KO_WIDE_PREFETCH
+        if (pf_late && i + 1 < n) wide_prefetch(kr, bkd + (size_t)(i + 1) * trgsw, w, t);
+#endif
+        if (is_inv) {
             C2 e[1][8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) e[0][q] = s_prod[0][w][t + 64 * br3(q)];
-            fft512<1, true, FU>(e, s_prod[0][w], T, t);
-            uint32_t *pa = s_acc + w * 1024;
+            for (int q = 0; q < 8; q++) e[0][q] = s_prod[0][ipoly][t + 64 * br3(q)];
+            C2 twr[8];  // untwist factors, read before the transform: their latency hides behind it
+#pragma unroll
+            for (int q = 0; q < 8; q++) twr[q] = twist_t[64 * q];
+            pp.mark(12);
+            fft512<1, true, FU>(e, s_prod[0][ipoly], T, t);
+            pp.mark(13);
+            uint32_t *pa = s_acc + ipoly * 1024;
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 double re, im;
-                untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-                pa[t + 64 * q] += to_torus<SMALL, FU>(re, near);
-                pa[t + 64 * q + 512] += to_torus<SMALL, FU>(im, near);
+                untwist_out<false, FU>(e[0][q], twr[q], re, im);
+                accr[q] += to_torus<SMALL, FU>(re, near);
+                accr[q + 8] += to_torus<SMALL, FU>(im, near);
+                pa[t + 64 * q] = accr[q];
+                pa[t + 64 * q + 512] = accr[q + 8];
             }
         }
         pp.mark(5);
@@ -2066,7 +2115,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     pp.mark(6);
 #ifdef TFHE_PHASE_PROF
     if (t == 0)
-        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[w * 8 + k], (unsigned long long)pp.acc[k]);
+        for (int k = 0; k < 16; k++) atomicAdd(&g_phase_cycles[w * 16 + k], (unsigned long long)pp.acc[k]);
 #endif
     if (FU) near_tie_flag(P, near, g, true);
 
