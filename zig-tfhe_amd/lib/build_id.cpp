@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "5b1f3d172f15b25d"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "bd07b1dca5d094c5"; }
