@@ -2,6 +2,7 @@
 // on a 1024-gate 128-bit batch with random operands (timing only, no parity).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DTFHE_PHASE_PROF \
 //         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
+#define TFHE_SINGLE_TU
 #include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
 
 #include <cstdio>

@@ -87,6 +87,11 @@ struct LaunchOpts {
 
 // ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------
 // idx: NULL, or B pairs (a, b) of ciphertext indices into in_a / in_b (circuit gather)
+// The default whole-form kernels (k_blind_rotate<L, true, true, true, true>), built in their
+// own unit with the max-memory-clause scheduler (tfhe_kernels_whole.hip).
+hipError_t launch_whole_default(int L, dim3 grid, dim3 block, hipStream_t s, const KParams &P, const DevTables &T,
+                                const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                                const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B);
 hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out,

@@ -1278,6 +1278,27 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     }
 }
 
+#ifdef TFHE_WHOLE_TU
+// tfhe_kernels_whole.hip: this file compiled a second time for the default
+// whole-form kernels only (loader waves, slot counters, fused arithmetic), with
+// hipcc's max-memory-clause machine scheduler (Makefile).  That scheduler
+// groups the kernel's LDS operations into clauses: 6.37-6.41 vs 6.48-6.55 ms per
+// 1,024 gates, alternating on two boxes, the same words
+// (profiles/r03r_ab_sched_strategy.txt).  Applied to the whole file it cost the
+// latency form 2 % (16-bit adder 101.5 vs 99.7 ms), hence the separate unit.
+hipError_t launch_whole_default(int L, dim3 grid, dim3 block, hipStream_t s, const KParams &P, const DevTables &T,
+                                const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                                const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B) {
+    switch (L) {
+    case 1: hipLaunchKernelGGL((k_blind_rotate<1, true, true, true, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B); break;
+    case 2: hipLaunchKernelGGL((k_blind_rotate<2, true, true, true, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B); break;
+    case 3: hipLaunchKernelGGL((k_blind_rotate<3, true, true, true, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#else  // the rest of the library's kernels and launchers
+
 // ---------------------------------------------------------------------------
 // Blind rotation, "octo" form (large batches): EIGHT items per 512-thread
 // workgroup, one wave each, so every SIMD runs two gate waves that both issue
@@ -2971,6 +2992,22 @@ static bool small_products(const KParams &P) {
     return std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 49);
 }
 
+// The default whole-form kernel lives in its own unit (launch_whole_default,
+// tfhe_kernels_whole.hip); single-file builds of this source (tools/phase_prof.hip,
+// tools/fft_bench.hip) define TFHE_SINGLE_TU and launch it here.
+#ifdef TFHE_SINGLE_TU
+#define WHOLE_DEFAULT_LAUNCH(L_, S_)                                                                              \
+    hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, S_, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,   \
+                       testvec, bk2, out, out_mode, B)
+#else
+#define WHOLE_DEFAULT_LAUNCH(L_, S_)                                                                              \
+    do {  /* fused implies SMALL: the kernel is never instantiated in this unit */                              \
+        if (!(S_)) return hipErrorInvalidValue;                                                                   \
+        const hipError_t e_ = launch_whole_default(L_, grid, block, s, P, T, ops, in_a, in_b, idx, testvec, bk2,  \
+                                                   out, out_mode, B);                                             \
+        if (e_ != hipSuccess) return e_;                                                                          \
+    } while (0)
+#endif
 static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T, const uint8_t *ops,
                                const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode, size_t B,
@@ -3052,8 +3089,7 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
                                idx, testvec, bk2, out, out_mode, B);                                              \
             if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ ",false> (split form)";                         \
         } else if (loader && fused && O.br_flags) {                                                               \
-            hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, S_, true>), grid, block, 0, s, P, T, ops, in_a, in_b,\
-                               idx, testvec, bk2, out, out_mode, B);                                              \
+            WHOLE_DEFAULT_LAUNCH(L_, S_);                                                                         \
             if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true,true,true> (whole form, loader waves, slot counters, fused)"; \
         } else if (loader && O.br_flags) {                                                                        \
             hipLaunchKernelGGL((k_blind_rotate<L_, S_, true, false, true>), grid, block, 0, s, P, T, ops, in_a,   \
@@ -3523,4 +3559,5 @@ hipError_t launch_bk_unpermute(const KParams &, const double *bkd, double *bk_re
     return hipGetLastError();
 }
 
+#endif  // TFHE_WHOLE_TU
 }  // namespace tfhe

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "bd07b1dca5d094c5"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "8f1f211af6f4c756"; }
