@@ -704,7 +704,9 @@ DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 
             fa[q] = c2(fa[q].x + ta.x, fa[q].y + ta.y);
             fb[q] = c2(fb[q].x + tb.x, fb[q].y + tb.y);
         }
+#ifndef TFHE_MAC_NO_FENCE
         __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 }
 
@@ -831,8 +833,15 @@ DEV bool lds_layout_bad(const void *smem) { return ((uint32_t)(size_t)(const lds
 // MACs (~9 k cycles) before its use, so the coarse poll never makes it late:
 // 7.39 -> 6.98 ms per 1,024 gates (sleep 1 at priority 3 before;
 // profiles/r02_ab_loader_poll.txt).
+// Round 3, under the max-memory-clause scheduler: s_sleep 96 (~6 k cycles)
+// instead of 12, alternating on 6 boxes: 6.21-6.35 vs 6.39-6.53 ms per 1,024
+// gates, 80-bit +2.6 %, 4,096 gates 27.3-27.9 vs 28.2-29.4 ms, the 65,536-gate
+// circuit 635-639 vs 655-669 ms.  Not monotonic in the sleep (48: 6.27-6.32,
+// 64: 6.53-6.58, 127: 6.31-6.33 ms): the poll period interacts with the pair
+// period, so this is a measured setting.  s_wakeup from the gate waves and a
+// fixed delay after the condition were slower (profiles/r03r_ab_loader_sleep.txt).
 #ifndef TFHE_LOADER_SLEEP
-#define TFHE_LOADER_SLEEP 12
+#define TFHE_LOADER_SLEEP 96
 #endif
 #ifndef TFHE_LOADER_PRIO
 #define TFHE_LOADER_PRIO 0

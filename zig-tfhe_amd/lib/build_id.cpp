@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "8f1f211af6f4c756"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "429fac9a75b08927"; }
