@@ -46,6 +46,9 @@ HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md chip table (spec)
 METRIC = "gate-bootstraps/sec (NAND, 128-bit params) at 1/2/4/8 MI355X; % HBM roofline"
 KERNEL_SRC = os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_kernels.hip")
 PMC_PATH = os.path.join(ROOT, "profiles", "pmc_blind_rotate.json")
+# rocprofv3 --kernel-trace --stats average of the blind-rotation kernel for the kernel
+# binary it was measured on (tools/rocprof_record.py writes it from a committed stats csv)
+ROCPROF_PATH = os.path.join(ROOT, "profiles", "rocprof_blind_rotate.json")
 REFERENCE_MS_PER_GATE = 37.31  # zig-tfhe's published single-thread gate time (CHANGELOG.md:86)
 
 
@@ -218,15 +221,38 @@ def rooflines(p, B, params, br_avg_s, kernel):
         f64_insts = pmc.get("valu_f64_insts_per_launch", 0) + pmc.get("valu_fma_f64_insts_per_launch", 0)
         if f64_insts:
             roof["pmc"]["valu_f64_frac_from_pmc"] = round(f64_insts * 64 / br_avg_s / VALU_F64_PEAK, 4)
+        # the DRAM side of the same kernel: measured bytes per launch / kernel time / HBM peak
+        roof["dram"] = {"achieved_gbs": round(pmc["hbm_bytes_per_launch"] / br_avg_s / 1e9, 1),
+                        "peak_gbs": HBM_PEAK_BPS / 1e9,
+                        "frac": round(pmc["hbm_bytes_per_launch"] / br_avg_s / HBM_PEAK_BPS, 4)}
     else:
         roof["traffic_note"] = why
+    # the same kernel's rocprofv3 --stats average, beside the HIP-event one above
+    rp, rwhy = rocprof_record()
+    if rp:
+        roof["kernel_avg_ms_rocprof"] = rp["avg_ms"]
+        roof["rocprof"] = {k: rp[k] for k in ("launches", "min_ms", "max_ms", "source") if k in rp}
+        roof["frac_rocprof"] = round(ops / (rp["avg_ms"] / 1e3) / VALU_F64_PEAK, 4)
+    else:
+        roof["rocprof_note"] = rwhy
     alg = algorithmic_bytes_per_gate(p) * B
-    hbm = {"bound": "hbm", "achieved": round(alg / br_avg_s / 1e9, 2), "peak": HBM_PEAK_BPS / 1e9, "unit": "GB/s",
-           "frac": round(alg / br_avg_s / HBM_PEAK_BPS, 4), "algorithmic_bytes_per_launch": alg,
-           "note": ("SURVEY §8d streamed-key model: BK bytes every gate consumes (n*2L*2*N*8 + I/O) / kernel time. "
-                    "The 4 gates of a workgroup share each BK row through LDS and the XCDs' L2s hold the key, so "
-                    "this counts key bytes consumed, not DRAM traffic (roofline.traffic is the measured DRAM bytes)")}
-    return roof, hbm
+    # SURVEY §8d's streamed-key figure is not a DRAM roofline for this kernel: the 4 gates
+    # of a workgroup share every BK row through LDS and the XCDs' L2s hold the key, so it
+    # counts key bytes CONSUMED per second (no fraction of the HBM peak is claimed for it;
+    # roofline.dram is the measured DRAM side)
+    key = {"key_bytes_consumed_per_s": round(alg / br_avg_s, 0), "key_bytes_consumed_per_launch": alg,
+           "note": "n*2L*2*N*8 + I/O bytes every gate consumes, / kernel time; on-chip reuse, not DRAM traffic"}
+    return roof, key
+
+
+def rocprof_record():
+    """profiles/rocprof_blind_rotate.json if it was measured on this kernel binary."""
+    if not os.path.exists(ROCPROF_PATH):
+        return None, "no rocprof record"
+    rec = json.load(open(ROCPROF_PATH))
+    if rec.get("kernel_build_id") != kernel_build_id():
+        return None, "rocprof record measured on another kernel binary (build id differs): not reported"
+    return rec, None
 
 
 def timed(fn, steps, warmup, world, device):
@@ -561,7 +587,7 @@ def main():
                                    f"(n={p.n}, N={p.N}, L={p.L}, Bg=2^{p.bgbit}, t={p.iks_t})",
                        "global_batch": total, "params": args.params, "parallelism": f"dp{world}"},
             "roofline": roof,
-            "roofline_hbm_accounting": hbm,
+            "key_bytes_consumed": hbm,
             "key_switch": {"kernel": " + ".join(kernels.split(" + ")[1:]), "avg_ms": round(ks_avg_s * 1e3, 3)},
             "margin_guard": {"recomputed_items": recomputed, "items": B * args.steps,
                              "note": "fused arithmetic; items that round a value 1/4 or more off its integer are "

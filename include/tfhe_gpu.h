@@ -130,7 +130,8 @@ int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
  * passes them to every device.  TFHE_ERR_INVALID for an unknown key or value. */
 enum {
     TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 2 split, 3 latency, 4 pair,
-                                     5 octo (8 items per workgroup, two gate waves per SIMD) */
+                                     5 octo (8 items per workgroup, two gate waves per SIMD), 6 duo (two
+                                     computing waves per item on one SIMD, no barriers in the step loop) */
     TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
     TFHE_OPT_KS_FORM = 3,         /* key switch: 3 auto (default: the one-hot GEMM on the matrix
                                      cores for basebit 2 and 5, else lanes), 0 lanes / ring,
@@ -155,20 +156,29 @@ enum {
                                      0 (default) one H2D -> kernels -> D2H sequence, 1 chunked through
                                      pinned staging on 4 streams (measured slower on the MI355X box,
                                      whose pageable copies run at ~50 GB/s: DESIGN.md §2.1) */
-    TFHE_OPT_CIRCUIT_SPLIT = 13   /* multi-device circuit_eval: 0 auto (default: connected components
+    TFHE_OPT_CIRCUIT_SPLIT = 13,  /* multi-device circuit_eval: 0 auto (default: connected components
                                      on devices, or by levels when one component dominates), 1
                                      components, 2 levels (each level's gates split over the devices,
                                      outputs all-gathered by peer copies before the next level) */
+    TFHE_OPT_FUSED_ADMITTED = 14  /* read-only (get_option): 1 if the resident cloud key passed the fused
+                                     arithmetic's admission check at load (largest BK spectrum component
+                                     <= 2^39), 0 if it was refused and TFHE_ARITH_AUTO
+                                     runs the reference's expression trees for it */
 };
 /* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
  * runs fused multiply-adds in the reference's operation order, with a margin
- * guard: every value it rounds must lie within 1/4 of an integer (the fused
- * and the reference's values differ by less than 1/8); an item
+ * guard: every value it rounds must lie within 1/4 of an integer; an item
  * that rounded anything further off is recomputed in the reference's
- * expression trees in the same stream (tfhe_gpu_near_tie_items counts them),
- * so both round to the same integers.  UINT4: the reference's trees.
- * TFHE_ARITH_REFERENCE: the reference's expression trees everywhere. */
-enum { TFHE_ARITH_AUTO = 0, TFHE_ARITH_REFERENCE = 1 };
+ * expression trees in the same stream (tfhe_gpu_near_tie_items counts them).
+ * Both round to the same integers while the fused and the reference's values
+ * differ by less than 1/4: an EMPIRICAL bound (measured max 0.094 on keygen'd
+ * keys), so a key is admitted to the fused arithmetic only
+ * when its BK lies in the measured regime (TFHE_OPT_FUSED_ADMITTED); other
+ * keys run the reference's trees.  UINT4: the reference's trees.
+ * TFHE_ARITH_REFERENCE: the reference's expression trees everywhere.
+ * TFHE_ARITH_FUSED_FORCED: fused (with the guard) even on a refused key —
+ * for tests of the margin guard only. */
+enum { TFHE_ARITH_AUTO = 0, TFHE_ARITH_REFERENCE = 1, TFHE_ARITH_FUSED_FORCED = 2 };
 /* The two libm candidates a Zig build of the reference can bind @cos/@sin to
  * (fft.zig:98-106, :591-593): glibc (linkLibC on Linux) or Zig's compiler_rt
  * port of the fdlibm/musl kernels.  DESIGN.md §6 lists the entries where the

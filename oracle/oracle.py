@@ -92,6 +92,7 @@ class Oracle:
         L.oracle_capture_rounded.restype = C.c_size_t
         L.oracle_capture_rounded.argtypes = [C.c_void_p, C.c_size_t]
         L.oracle_set_fused.argtypes = [C.c_int]
+        L.oracle_set_regroup.argtypes = [C.c_int]
         L.oracle_get_fused.restype = C.c_int
 
     # ---- cos/sin source of the twiddles (0 glibc, 1 fdlibm/musl; tfhe_oracle.c)
@@ -107,6 +108,11 @@ class Oracle:
         margin guard, a blind rotation that rounds near a tie redone in the
         reference's trees (the MI355X default at the 128/80-bit sets)."""
         self.lib.oracle_set_fused(2 if fused == 2 else int(bool(fused)))
+
+    def set_regroup(self, on: bool):
+        """Fused mode only: each output's MAC as (rows of a) + (rows of b), two
+        fma chains from 0.0 added once (the pair and duo kernel forms)."""
+        self.lib.oracle_set_regroup(int(bool(on)))
 
     def rounded_values(self, fn, cap=1 << 16):
         """Run fn() and return the pre-rounding values its inverse transforms

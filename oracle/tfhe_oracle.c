@@ -245,6 +245,12 @@ double oracle_trig_sin(double x, int source) { return source == 1 ? fd_sin(x) : 
  * kernel) is redone in the reference's trees — the MI355X default.  FUSED is
  * the arithmetic in force on this thread (a guarded recompute forces 0). */
 static int g_fused = 0, g_guard = 0;
+/* Regrouped row sums (the MI355X pair and duo forms):
+ * in fused mode each output's MAC is two fma chains from 0.0, one over the
+ * rows of a (0..L-1) and one over the rows of b (L..2L-1), added once at the
+ * end, instead of one chain over rows 0..2L-1. */
+static int g_regroup = 0;
+void oracle_set_regroup(int on) { g_regroup = on ? 1 : 0; }
 static __thread int tl_force_ref = 0, tl_near = 0;
 #define FUSED (g_fused && !tl_force_ref)
 void oracle_set_fused(int fused) {
@@ -549,10 +555,24 @@ void oracle_external_product(const oracle_params *p, const double *trgsw_fft,
     double *out_b = (double *)calloc(N, sizeof(double));
     oracle_decomposition(p, trlwe, offset, dec);
     for (uint32_t r = 0; r < R; r++) oracle_ifft(N, dec + (size_t)r * N, dec_fft + (size_t)r * N);
+    if (FUSED && g_regroup) {  /* (rows 0..L-1) + (rows L..2L-1), each chain from 0.0 */
+        double *hi_a = (double *)calloc(N, sizeof(double)), *hi_b = (double *)calloc(N, sizeof(double));
+        for (uint32_t r = 0; r < R; r++) {
+            const double *row = trgsw_fft + (size_t)r * 2 * N;
+            fma_in_fd(N / 2, r < p->L ? out_a : hi_a, dec_fft + (size_t)r * N, row);
+            fma_in_fd(N / 2, r < p->L ? out_b : hi_b, dec_fft + (size_t)r * N, row + N);
+        }
+        for (uint32_t i = 0; i < N; i++) {
+            out_a[i] = out_a[i] + hi_a[i];
+            out_b[i] = out_b[i] + hi_b[i];
+        }
+        free(hi_a); free(hi_b);
+    } else {
     for (uint32_t r = 0; r < R; r++) {
         const double *row = trgsw_fft + (size_t)r * 2 * N;
         fma_in_fd(N / 2, out_a, dec_fft + (size_t)r * N, row);
         fma_in_fd(N / 2, out_b, dec_fft + (size_t)r * N, row + N);
+    }
     }
     oracle_fft(N, out_a, out);
     oracle_fft(N, out_b, out + N);

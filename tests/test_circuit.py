@@ -38,12 +38,15 @@ def test_circuit_builder_wires():
 
 
 @pytest.mark.gpu
-def test_circuit_adder_16bit_bit_exact(oracle):
-    """402 + 304 = 706 through one circuit launch sequence; every output word
-    equals the reference's gate-by-gate evaluation (80-bit keys)."""
+@pytest.mark.parametrize("pname", ["80", "128"])
+def test_circuit_adder_16bit_bit_exact(oracle, pname):
+    """402 + 304 = 706 through one circuit launch sequence; every one of the 17
+    output words equals the reference's gate-by-gate evaluation.  "128" is
+    BASELINE config 3 at its stated parameter set (examples/add_two_numbers.zig:
+    24-73, 102-105): 80 oracle bootstraps, a few seconds of CPU."""
     from conftest import get_keys
-    k = get_keys(oracle, "80")
-    ctx = tfhe_amd.Context("80", 0)
+    k = get_keys(oracle, pname)
+    ctx = tfhe_amd.Context(pname, 0)
     ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
     sk = tfhe_amd.SecretKey(ctx.params, k.k0, k.k1)
     c = Circuit()

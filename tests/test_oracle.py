@@ -232,16 +232,19 @@ def _tmp_with_fields(oracle, p, fields):
 
 def _ext_values(oracle, p, rows, x, mode):
     """Pre-rounding values and words of externalProductWithFft with integer rows
-    (2L, 2, N) in `mode` (0 reference trees, 1 fused)."""
+    (2L, 2, N) in `mode` (0 reference trees, 1 fused, 3 fused with the pair / duo
+    forms' regrouped row sums)."""
     off = oracle.decomposition_offset(p)
     trgsw = np.array([[oracle.ifft((r[0] % (1 << 32)).astype(np.uint32)),
                        oracle.ifft((r[1] % (1 << 32)).astype(np.uint32))] for r in rows])
     try:
-        oracle.set_fused(mode)
+        oracle.set_fused(1 if mode == 3 else mode)
+        oracle.set_regroup(mode == 3)
         out = {}
         v = oracle.rounded_values(lambda: out.setdefault("w", oracle.external_product(p, trgsw, x, off)))
     finally:
         oracle.set_fused(0)
+        oracle.set_regroup(False)
     return v, out["w"]
 
 
@@ -322,6 +325,7 @@ def test_aligned_adversarial_digits_part_the_trees(oracle):
         return ((v - off) % (1 << 32)).astype(np.uint32)
 
     delta, part, mag = 0.0, 0, 0
+    delta_rg, part_rg = 0.0, 0  # the pair / duo forms' regrouped sums
     for trial in range(400):
         rows = g.integers(-(1 << 31), 1 << 31, (2 * p.L, 2, 1024))
         k = int(g.integers(0, 1024))
@@ -338,9 +342,74 @@ def test_aligned_adversarial_digits_part_the_trees(oracle):
         # the kernel's guard: v + (1.5*2^51 + 1/2) by one f64 add, mantissa bit 0 == 0
         near = ((v1 + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0
         assert not (differ & ~near).any()  # every parting coefficient is flagged
+        if trial % 4 == 0:
+            v3, w3 = _ext_values(oracle, p, rows, x, 3)
+            delta_rg = max(delta_rg, float(np.abs(v0 - v3).max()))
+            differ3 = w0 != w3
+            part_rg += int(differ3.sum())
+            near3 = ((v3 + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0
+            assert not (differ3 & ~near3).any()
     assert mag > 2 ** 47.5
     assert delta < 0.125  # half the guard's 1/4 margin
     assert part > 0
+    assert delta_rg < 0.125
+
+
+FUSED_BK_SPECTRUM_MAX = 2.0 ** 39  # tfhe_gpu.cpp key_admission
+
+
+@pytest.mark.parametrize("kind", ["keygen_like", "max_magnitude", "sparse", "spike", "low_frequency", "constant"])
+def test_key_admission_structured_rows(oracle, kind):
+    """structured BK rows against the key admission rule.  For
+    each kind, either the admission refuses the key (largest BK spectrum component
+    past 2^39: the kernels then run the reference's trees), or, against
+    sign-aligned adversarial digits (the worst the public key allows), the fused
+    and the regrouped fused values stay within 0.15 of the reference's (below the
+    guard's 1/4) and every coefficient where the words part is flagged by the
+    guard's one-add test, so guarded-fused equals reference."""
+    from oracle import params
+    p = params("128")
+    off = oracle.decomposition_offset(p)
+    g = rng(909)
+    R = (1 << 31) - 1
+    kinds = {
+        "keygen_like": lambda: g.integers(-(1 << 31), 1 << 31, (6, 2, 1024)),
+        "max_magnitude": lambda: np.where(g.random((6, 2, 1024)) < 0.5, R, -R),
+        "sparse": lambda: np.where(g.random((6, 2, 1024)) < 16 / 1024, g.integers(-(1 << 31), 1 << 31, (6, 2, 1024)), 0),
+        "spike": lambda: np.array([[np.eye(1, 1024, int(g.integers(0, 1024)))[0] * R for _ in range(2)]
+                                   for _ in range(6)]).astype(np.int64),
+        "low_frequency": lambda: np.round(R * np.cos(2 * np.pi * np.arange(1024) * 3 / 2048
+                                                     + g.random((6, 2, 1)) * 6)).astype(np.int64),
+        "constant": lambda: np.full((6, 2, 1024), R, np.int64),
+    }
+
+    def tmp3(f0, f1, f2):
+        v = (f0.astype(np.uint64) << 26) | (f1.astype(np.uint64) << 20) | (f2.astype(np.uint64) << 14)
+        return ((v - off) % (1 << 32)).astype(np.uint32)
+
+    admitted_all, delta = True, 0.0
+    for trial in range(12):
+        rows = kinds[kind]()
+        spec = max(np.abs(oracle.ifft((r % (1 << 32)).astype(np.uint32))).max() for rr in rows for r in rr)
+        if spec > FUSED_BK_SPECTRUM_MAX:
+            admitted_all = False
+            continue
+        k = int(g.integers(0, 1024))
+        j = np.arange(1024)
+        m, w = (k - j) % 1024, np.where(j <= k, 1, -1)
+        F = [np.where(w * np.sign(rows[i][trial % 2][m]) >= 0, 63, 0) for i in range(6)]
+        x = np.concatenate([tmp3(F[0], F[1], F[2]), tmp3(F[3], F[4], F[5])])
+        v0, w0 = _ext_values(oracle, p, rows, x, 0)
+        for mode in (1, 3):
+            v, wv = _ext_values(oracle, p, rows, x, mode)
+            delta = max(delta, float(np.abs(v0 - v).max()))
+            near = ((v + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0
+            assert not ((w0 != wv) & ~near).any()
+    if kind in ("low_frequency", "constant"):
+        assert not admitted_all  # concentrated spectra: 2^40.4-2^41.3, refused
+    if kind in ("keygen_like", "sparse", "spike"):
+        assert admitted_all
+    assert delta < 0.15
 
 
 def test_guarded_fused_rotation_equals_reference_on_a_crafted_near_tie(oracle):

@@ -47,7 +47,7 @@ int main(int argc, char **argv) {
         CK(hipEventRecord(e0));
         LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
         const char *form = argc > 2 ? argv[2] : "whole";
-        O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
+        O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : form[0] == 'd' ? 6 : 1;
         if (argc > 3) O.br_flags = atoi(argv[3]);  // whole form: 1 slot counters, 0 barriers
         CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
         CK(hipEventRecord(e1));
@@ -65,6 +65,17 @@ int main(int argc, char **argv) {
                 for (int w = 0; w < 8; w++) printf(" %8.1f", c[w * 16 + k] / (double)B / P.n);
                 printf("\n");
             }
+            continue;
+        }
+        if (O.br_form == 6) {  // duo form: 2 waves per gate; phases summed over both waves
+            const char *dn[8] = {"gather+tmp", "digits+fwd fft", "refill wait", "dma issue+vmcnt", "pub wait",
+                                 "mac", "hand-off", "inverse+acc"};
+            double tot = 0;
+            for (int k = 0; k < 8; k++) tot += c[k];
+            printf("rep %d: %.3f ms; duo form, s_memtime ticks per wave-step:\n", rep, ms);
+            for (int k = 0; k < 8; k++)
+                printf("  %-16s %10.1f  %5.1f%%\n", dn[k], c[k] / (2.0 * B) / P.n, 100.0 * c[k] / tot);
+            printf("  total            %10.1f\n", tot / (2.0 * B) / P.n);
             continue;
         }
         const char *nm[8] = {"tmp", "fwd-fft(pairs)", "barrier1", "mac", "barrier2", "inverse+add", "tail", "dma-issue"};

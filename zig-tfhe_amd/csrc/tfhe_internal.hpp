@@ -31,9 +31,12 @@ struct KParams {
     uint32_t spin_cap;  // polls before a slot-counter wait gives up (TFHE_OPT_BR_SPIN_CAP; 0 = default)
     // Near-tie flags of the fused arithmetic's margin guard,
     // one byte per item of a blind-rotation launch, all zero between launches:
-    // a fused kernel sets tie_flags[g] when item g rounded a value within 1/8 of
-    // a tie; the reference-tree recompute launched after it (fallback = 1) redoes
-    // the flagged items' workgroups and clears their flags.
+    // a fused kernel sets tie_flags[g] when item g rounded a value 1/4 or more off
+    // its integer (within 1/4 of a tie); the reference-tree recompute launched
+    // after it (fallback = 1) redoes the flagged items' workgroups and clears
+    // their flags.  Sound while |v_fused - v_reference| < 1/4: measured max 0.094
+    // on keygen'd keys, an empirical bound; keys outside that regime are refused
+    // the fused arithmetic at load (key admission).
     uint8_t *tie_flags;
     int fallback;
 };
@@ -82,8 +85,15 @@ struct LaunchOpts {
     int ks_groups = 0;   // basebit >= 5: item groups per block (0 auto = 4; 1, 2, 4, 8)
     int ks_sel_items = 8;  // select/gather form: items per block (8, 16, 32)
     int arith_strict = 0;  // 1: the reference's f64 expression trees even where fused multiply-adds round
-                           // to the same integers (the L=3 / Bg=2^6 sets)
+                           // to the same integers (the L=3 / Bg=2^6 sets); 2: fused even on
+                           // a key the admission check refused (margin-guard tests only)
+    int key_fused_ok = 1;  // the resident BK passed the fused arithmetic's admission check
 };
+// The fused arithmetic runs unless the reference's trees are requested, and only on
+// an admitted key unless forced (TFHE_OPT_ARITH, LaunchOpts::key_fused_ok).
+inline bool fused_allowed(const LaunchOpts &O) {
+    return O.arith_strict == 2 || (O.arith_strict == 0 && O.key_fused_ok != 0);
+}
 
 // ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------
 // idx: NULL, or B pairs (a, b) of ciphertext indices into in_a / in_b (circuit gather)
@@ -150,6 +160,7 @@ hipError_t launch_bk_permute(const KParams &P, const double *bk_ref, double *bkd
                              hipStream_t s);
 // 64-bit fingerprint of bytes (a multiple of 16) at p into *out (device), async
 hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s);
+hipError_t launch_absmax(const double *p, size_t count, unsigned long long *out, hipStream_t s);
 hipError_t launch_bk_unpermute(const KParams &P, const double *bkd, double *bk_ref, size_t rows,
                                hipStream_t s);
 

@@ -1943,6 +1943,384 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
 }
 
 // ---------------------------------------------------------------------------
+// Blind rotation, "duo" form (round 4): TWO computing waves per item on ONE
+// SIMD, 4 items per 512-thread workgroup, so a 1,024-item batch (one item per
+// SIMD) runs two f64 instruction streams on every SIMD instead of one (the
+// whole form's gate wave issues f64 at ~2.6 ns per instruction alone, ~2.1
+// with a second computing wave beside it).  Wave (g, h) owns
+// accumulator polynomial h (0: a, 1: b) and its L decomposition rows:
+//   1. rotation gather of its own polynomial from its own LDS buffer (the
+//      rotation never mixes the polynomials) -> tmp words in registers;
+//   2. per level l: digits, one forward FFT, and the MAC of row hL + l against
+//      both output parts into partial sums P_h,a / P_h,b (fused chains from
+//      0.0, rows in the reference's order within each half);
+//   3. hand-off: P_h,(1-h) goes into the partner's buffer once the partner's
+//      forward FFTs are done (an LDS counter per wave), the partner's partial
+//      comes back into its own buffer; output h = P_0,h + P_1,h (the pair
+//      form's regrouped sum, exact-integer regime only: DESIGN.md §6.1);
+//   4. inverse FFT of output h, untwist, guarded conversion, acc_h update.
+// No workgroup barrier in the step loop.  BK level slots (rows l and L+l of
+// one BK[i], 32 KB) double-buffered and shared by the 8 waves; every wave
+// issues its 4 x 1 KB share of each level's LDS-DMA right after its forward
+// FFT of the level before, publishes it (pub) once landed,
+// and a refill waits until all 8 waves are done with the slot (done).  Every
+// wait is a bounded poll (spin_until_ge).
+// LDS: BK 2 x 32 KB + tables 16 KB + 8 wave buffers x 8 KB (accumulator copy /
+// FFT exchange / hand-off) + 4 x 2 KB a~ + counters = 152 KB.
+// ---------------------------------------------------------------------------
+constexpr int BD_GATES = 4;
+constexpr int BD_WAVES = 2 * BD_GATES;
+constexpr int BD_LDS_BK = 2 * 2048 * 16;  // two level slots of rows (l, L+l), double2
+constexpr int BD_LDS_BUF = 512 * 16;      // per wave
+constexpr int BD_LDS_AT = 1024 * 2;       // per item
+constexpr int BD_LDS_SYNC = 128;          // pub[2] done[2] fwd[8] hand[8] bt[4]
+constexpr int BD_LDS_BUF_AT = BD_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;
+constexpr int BD_LDS_TOTAL = BD_LDS_BUF_AT + BD_WAVES * BD_LDS_BUF + BD_GATES * BD_LDS_AT + BD_LDS_SYNC;
+static_assert(BD_LDS_TOTAL <= 160 * 1024, "duo form LDS");
+static_assert(BD_LDS_BUF_AT % 4096 == 0 && BD_LDS_BUF % 4096 == 0, "gather_rot1 needs 4 KB-aligned buffers");
+
+// Rotation gather of ONE polynomial (1,024 words at the 4 KB-aligned byte
+// address `base`): lane word m = coefficient t + 64m of X^a~ * p, sign in bit
+// 12 of xb[m] (gather_sign), as gather_rot.
+DEV void gather_rot1(uint32_t base, int t, int at, uint32_t *xb, uint32_t *v) {
+    const uint32_t rbb = (uint32_t)((t - at) & 2047) << 2;
+    const uint32_t mask = __builtin_amdgcn_readfirstlane(0xFFCu);
+    uint32_t vmask;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(vmask) : "s"(mask));
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        xb[m] = rbb + 256u * m;
+        uint32_t a;
+        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(xb[m]), "v"(vmask), "s"(base));
+        v[m] = lds_read_u32(a);
+    }
+}
+
+// One level's whole LDS-DMA by ONE wave (duo form, claimed by the wave that
+// found the slot free first): the level slot holds row lo (the a polynomial's
+// row, 16 KB) then row hi (the b polynomial's), 32 pieces of 1 KB; SGPR base
+// per piece + the lane's 16-B offset, hand-counted completion (vmcnt).
+DEV void issue_level_full(const double2 *__restrict__ row_lo, const double2 *__restrict__ row_hi, double2 *slot,
+                          int t) {
+    const uint32_t base = (uint32_t)(size_t)(lds_void_t *)slot;
+    const uint32_t voff = (uint32_t)t * 16u;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+        const double2 *piece = (j < 16 ? row_lo : row_hi) + (j & 15) * 64;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(base + 1024u * (uint32_t)j);
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(dst), "s"(piece)
+            : "memory");
+    }
+}
+
+// ds_cmpst_rtn_b32 by lane 0 (if *p == cmp: *p = val); the old value, uniform.
+DEV uint32_t lds_cas_u32(uint32_t *p, uint32_t cmp, uint32_t val) {
+    const uint32_t addr = (uint32_t)(size_t)(lds_void_t *)p;
+    uint32_t old;
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "ds_cmpst_rtn_b32 %[old], %[addr], %[cmp], %[val]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [old] "=&v"(old), [save] "=&s"(save)
+        : [addr] "v"(addr), [cmp] "v"(cmp), [val] "v"(val)
+        : "memory");
+    return __builtin_amdgcn_readfirstlane(old);
+}
+// A plain LDS word read, uniform (polled counters).
+DEV uint32_t lds_peek_u32(const uint32_t *p) {
+    const uint32_t addr = (uint32_t)(size_t)(const lds_void_t *)p;
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// MAC of one row for the duo form's two partial sums: `po` takes the part at
+// bk_own, `px` the part at bk_oth ([q][a|b][lane] rows: the two parts of
+// frequency group q at (2q)*64 and (2q+1)*64), BK words two groups ahead.
+template <bool FU>
+DEV void mac_row_roles(C2 *po, C2 *px, const C2 *d, const double2 *bk_own, const double2 *bk_oth, int t) {
+    double2 k[3][2];
+    k[0][0] = bk_own[t];
+    k[0][1] = bk_oth[t];
+    k[1][0] = bk_own[128 + t];
+    k[1][1] = bk_oth[128 + t];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        if (q + 2 < 8) {
+            k[(q + 2) % 3][0] = bk_own[(q + 2) * 128 + t];
+            k[(q + 2) % 3][1] = bk_oth[(q + 2) * 128 + t];
+        }
+        const C2 x = d[q];
+        const double2 ko = k[q % 3][0], kx = k[q % 3][1];
+        if (FU) {
+            po[q] = c2(fmad(x.x, ko.x, fmad(-x.y, ko.y, po[q].x)), fmad(x.x, ko.y, fmad(x.y, ko.x, po[q].y)));
+            px[q] = c2(fmad(x.x, kx.x, fmad(-x.y, kx.y, px[q].x)), fmad(x.x, kx.y, fmad(x.y, kx.x, px[q].y)));
+        } else {
+            const C2 to = c2(x.x * ko.x - x.y * ko.y, x.x * ko.y + x.y * ko.x);
+            const C2 tx = c2(x.x * kx.x - x.y * kx.y, x.x * kx.y + x.y * kx.x);
+            po[q] = c2(po[q].x + to.x, po[q].y + to.y);
+            px[q] = c2(px[q].x + tx.x, px[q].y + tx.y);
+        }
+    }
+}
+
+#ifndef TFHE_DUO_EX2_REGS  // A/B: 1 = exchange 2 of every transform by permlane / DPP moves (ex2_regs)
+#define TFHE_DUO_EX2_REGS 0
+#endif
+
+template <int L, bool SMALL, bool FU>
+__global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
+    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
+    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
+    static_assert(FU || L == 1, "regrouped row sums need the exact-integer regime");
+    constexpr bool EX2LDS = TFHE_DUO_EX2_REGS == 0;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[BD_LDS_TOTAL];
+    const int tid = threadIdx.x;
+    const int t = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int gs = w & 3;  // item slot: waves gs and gs + 4 share a SIMD
+    const int h = w >> 2;  // polynomial owned by this wave
+    const int pw = w ^ 4;  // partner wave
+    double2 *s_bk = reinterpret_cast<double2 *>(smem);
+    C2 *s_tw = reinterpret_cast<C2 *>(smem + BD_LDS_BK);
+    C2 *s_twist = reinterpret_cast<C2 *>(smem + BD_LDS_BK + BR_LDS_TW);
+    unsigned char *bufs = smem + BD_LDS_BUF_AT;
+    uint32_t *s_buf = reinterpret_cast<uint32_t *>(bufs + w * BD_LDS_BUF);
+    C2 *s_x = reinterpret_cast<C2 *>(s_buf);
+    C2 *s_xp = reinterpret_cast<C2 *>(bufs + pw * BD_LDS_BUF);  // partner's buffer (hand-off target)
+    uint16_t *s_at = reinterpret_cast<uint16_t *>(bufs + BD_WAVES * BD_LDS_BUF + gs * BD_LDS_AT);
+    uint32_t *s_sync = reinterpret_cast<uint32_t *>(smem + BD_LDS_TOTAL - BD_LDS_SYNC);
+    uint32_t *s_pub = s_sync, *s_done = s_sync + 2, *s_fwd = s_sync + 4, *s_hand = s_sync + 12, *s_cl = s_sync + 24;
+    int *s_bt = reinterpret_cast<int *>(s_sync + 20);
+
+    if (lds_layout_bad(smem)) {
+        if (tid == 0) __hip_atomic_fetch_or(P.err, (uint32_t)DEV_ERR_LDS_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const int n = P.n;
+    const size_t g_raw = (size_t)blockIdx.x * BD_GATES + gs;
+    const bool valid = g_raw < B;
+    const size_t g = valid ? g_raw : B - 1;  // ragged tail: compute a copy, store nothing
+    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
+    const uint32_t *A = in_a + ia * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
+    const int op = ops ? (int)ops[g] : 255;
+    const size_t step = (size_t)2 * L * 1024;  // double2 per BK[i]
+    const uint32_t levels = (uint32_t)n * L;
+
+    auto level_lo = [&](uint32_t k) { return bkd + (size_t)(k / L) * step + (size_t)(k % L) * 1024; };
+    auto level_hi = [&](uint32_t k) { return bkd + (size_t)(k / L) * step + (size_t)(L + k % L) * 1024; };
+    if (w == 0) {  // levels 0 and 1 (claimed: cl = 2) and the zeroed counters
+        issue_level_full(level_lo(0), level_hi(0), s_bk, t);
+        if (levels > 1) issue_level_full(level_lo(1), level_hi(1), s_bk + 2048, t);
+        if (t < 20) s_sync[t] = 0u;  // pub, done, fwd, hand (bt: written by the h = 0 waves)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (t == 0) {
+            s_pub[0] = 1u;
+            s_pub[1] = levels > 1 ? 1u : 0u;
+            *s_cl = levels > 1 ? 2u : 1u;
+        }
+    }
+    for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
+    if (h == 0) {  // a~_i, b~ (trgsw.zig:297, :312), 64-bit adds
+        for (int i = t; i <= n; i += 64) {
+            const uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
+            const uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
+            if (i < n) s_at[i] = (uint16_t)tl;
+            else s_bt[gs] = 2048 - (int)tl;
+        }
+    }
+    __syncthreads();  // tables, a~, b~ and the zeroed counters visible to every wave
+    const int bt = __builtin_amdgcn_readfirstlane(s_bt[gs]);
+    uint32_t acc[16];  // acc_h = X^{b~} * testvec_h (trgsw.zig:300-306), lane word m = coefficient t + 64m
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        acc[m] = rot_read(testvec + h * 1024, t + 64 * m, bt);
+        s_buf[t + 64 * m] = acc[m];
+    }
+    wave_sync();
+    LdsTwAtPass T;
+    T.init(s_tw, TT);
+    const C2 *twist_t = s_twist + t;
+    int at_next = s_at[0];
+    uint32_t near = NEAR_NONE;
+    uint32_t fail = 0;
+    // after one wait gave up (wrong words follow, reported through the device
+    // error word), every later wait polls once: a broken protocol ends fast
+    const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
+    const uint32_t msbs = digit_msbs(L, P.bgbit);
+    const uint32_t buf_base = (uint32_t)(size_t)(lds_void_t *)s_buf;  // 4 KB-aligned (BD_LDS_BUF_AT)
+    // BK levels this wave claimed and has not published yet (at most two: k and k + 1)
+    uint32_t owe0 = ~0u, owe1 = ~0u;
+    auto publish_owed = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my claimed levels' pieces landed
+        if (owe0 != ~0u) counter_add(s_pub + (owe0 & 1));
+        if (owe1 != ~0u) counter_add(s_pub + (owe1 & 1));
+        owe0 = owe1 = ~0u;
+    };
+    // claim level j (the next unclaimed, cl == j) if its slot is free (all 8 waves done with
+    // level j - 2) and issue its whole DMA; false if the slot is busy or another wave won it
+    auto try_claim = [&](uint32_t j) {
+        if (j >= levels || lds_peek_u32(s_done + (j & 1)) < 8u * (j >> 1)) return false;
+        if (lds_cas_u32(s_cl, j, j + 1) != j) return false;
+        issue_level_full(level_lo(j), level_hi(j), s_bk + (j & 1) * 2048, t);
+        if (owe0 == ~0u) owe0 = j;
+        else owe1 = j;
+        return true;
+    };
+
+    PhaseProf pp;  // TFHE_PHASE_PROF (tools/phase_prof.hip): per-phase s_memtime per wave
+    pp.start();
+    for (int i = 0; i < n; i++) {
+        pp.mark(0);
+        const int at = __builtin_amdgcn_readfirstlane(at_next);
+        at_next = s_at[i + 1 < n ? i + 1 : i];
+        // tmp_h = X^{a~} acc_h - acc_h + offset (flipped digit fields), in registers
+        uint32_t tmp[16], xb[16];
+        gather_rot1(buf_base, t, at, xb, tmp);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            const uint32_t sg = gather_sign(xb[m]), off_s = P.offset - sg;
+            tmp[m] = tmp_word(tmp[m], sg, off_s, acc[m], msbs);
+        }
+        wave_sync();  // the gather's reads precede the exchanges' writes into the buffer
+        // partial sums over this wave's rows: po for output h (kept), px for
+        // output 1 - h (handed to the partner); fmaInFd1024 accumulates from 0.0
+        C2 po[8], px[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            po[q] = c2(0.0, 0.0);
+            px[q] = c2(0.0, 0.0);
+        }
+        pp.mark(1);
+#pragma unroll 1
+        for (int l = 0; l < L; l++) {
+            const uint32_t k = (uint32_t)(L * i + l);  // level k of the launch lives in slot k & 1
+            C2 d[1][8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int m = br3(q);
+                d[0][q] = twist_in<FU>(digit_f64_flipped(tmp[m], l, P.bgbit), digit_f64_flipped(tmp[m + 8], l, P.bgbit),
+                                       twist_t[64 * m]);
+            }
+#ifndef TFHE_KO_FFT
+            fft512<1, false, FU, LdsTwAtPass, EX2LDS>(d, s_x, T, t);
+#endif
+            if (l == L - 1) counter_add(s_fwd + w);  // my exchanges are done: the partner may write my buffer
+            pp.mark(2);
+            // checkpoint: publish the levels I claimed (they had a forward FFT's time to
+            // land), then claim levels k and k + 1 if their slots are free and nobody has
+            if (owe0 != ~0u) publish_owed();
+            pp.mark(3);
+            {
+                uint32_t c = lds_peek_u32(s_cl);
+                if (c == k && try_claim(k)) c = k + 1;
+                if (c == k + 1) try_claim(k + 1);
+            }
+            if (owe0 == k) publish_owed();  // I claimed level k only now: it must land before my MAC
+            pp.mark(4);
+            // level k published (by its claimer); if nobody could claim it (slot busy), claim it here
+            {
+                uint32_t cap = fail ? 1u : spin_cap;
+                while (lds_peek_u32(s_pub + (k & 1)) < (k >> 1) + 1u) {
+                    if (lds_peek_u32(s_cl) == k && try_claim(k)) {
+                        publish_owed();
+                        continue;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    if (--cap == 0) {
+                        fail = 1;
+                        break;
+                    }
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            pp.mark(5);
+#ifndef TFHE_KO_MAC
+            // row hL + l, parts [q][a|b][lane]: output h's part at +64h, the other's at +64(1-h)
+            mac_row_roles<FU>(po, px, d[0], s_bk + (k & 1) * 2048 + h * 1024 + 64 * h, s_bk + (k & 1) * 2048 + h * 1024 + 64 * (1 - h), t);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+            counter_add(s_done + (k & 1));
+            pp.mark(1);
+        }
+        pp.mark(6);
+        // hand-off: P_h,(1-h) into the partner's buffer, the partner's into mine
+        spin_until_ge(s_fwd + pw, (uint32_t)i + 1u, fail ? 1u : spin_cap, fail);
+#pragma unroll
+        for (int q = 0; q < 8; q++) s_xp[t + 64 * q] = px[q];
+        counter_add(s_hand + w);
+        spin_until_ge(s_hand + pw, (uint32_t)i + 1u, fail ? 1u : spin_cap, fail);
+        __builtin_amdgcn_sched_barrier(0);
+        // output h = (rows 0..L-1) + (rows L..2L-1); IEEE addition commutes, so
+        // mine + other is that sum for either h
+        C2 e[1][8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int m = br3(q);
+            const C2 o = s_x[t + 64 * m];
+            const C2 mine = po[m];
+            e[0][q] = c2(mine.x + o.x, mine.y + o.y);
+        }
+        wave_sync();  // the partial's reads precede the inverse's exchange writes
+        pp.mark(7);
+#ifndef TFHE_KO_INV
+        fft512<1, true, FU, LdsTwAtPass, EX2LDS>(e, s_x, T, t);
+#endif
+        uint32_t nq[2] = {NEAR_NONE, NEAR_NONE};
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            double re, im;
+            untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
+            acc[q] += to_torus<SMALL, FU>(re, nq[0]);
+            acc[q + 8] += to_torus<SMALL, FU>(im, nq[1]);
+        }
+        near &= nq[0] & nq[1];
+        wave_sync();
+#pragma unroll
+        for (int m = 0; m < 16; m++) s_buf[t + 64 * m] = acc[m];
+        wave_sync();
+    }
+    pp.mark(0);
+#ifdef TFHE_PHASE_PROF
+    if (t == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], (unsigned long long)pp.acc[k]);
+#endif
+    report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
+    if (FU) near_tie_flag(P, near, g, valid);
+
+    if (!valid) return;
+    if (out_mode == BR_OUT_LV1) {  // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
+        uint32_t *o = out + g * (size_t)1025;
+        if (h == 0) {
+            for (int j = t; j < 1024; j += 64) o[j] = j == 0 ? s_buf[0] : 0u - s_buf[1024 - j];
+        } else if (t == 0) {
+            o[1024] = s_buf[0];
+        }
+    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {  // sampleExtractIndex2 (trlwe.zig:165-180)
+        uint32_t *o = out + g * (size_t)(n + 1);
+        if (h == 0) {
+            for (int j = t; j < n; j += 64) o[j] = j == 0 ? s_buf[0] : 0u - s_buf[n - j];
+        } else if (t == 0) {
+            o[n] = s_buf[0];
+        }
+    } else {
+        uint32_t *o = out + g * (size_t)2048 + h * 1024;
+        for (int j = t; j < 1024; j += 64) o[j] = s_buf[j];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Blind rotation, latency form ("wide"): ONE item per 512-thread workgroup,
 // for batches too small to give every SIMD a gate (circuit levels, single
 // gates).  Per CMUX step:
@@ -3031,7 +3409,7 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     const bool loader = !wide && !split && O.br_loader != 0;
     // fused arithmetic in the exact-integer regime (SMALL) unless the
     // reference expression trees are requested (TFHE_OPT_ARITH)
-    const bool fused = small && O.arith_strict == 0;
+    const bool fused = small && fused_allowed(O);
     if (form == 'o') {  // octo form: 8 items per workgroup, two gate waves per SIMD
         const dim3 grid((unsigned)((B + BO_GATES - 1) / BO_GATES)), block(64 * BO_GATES);
 #define BO_LAUNCH(L_, S_)                                                                                            \
@@ -3054,6 +3432,27 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
         }
 #undef BO_LAUNCH
         return hipGetLastError();
+    }
+    if (form == 'd') {  // duo form (2 computing waves per item); falls back to the whole form where not exact
+        const dim3 grid((unsigned)((B + BD_GATES - 1) / BD_GATES)), block(64 * BD_WAVES);
+        bool ok = true;
+        if (P.L == 3 && small && fused) {
+            hipLaunchKernelGGL((k_blind_rotate_duo<3, true, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,
+                               testvec, bk2, out, out_mode, B);
+            if (used) *used = "k_blind_rotate_duo<3,true,true> (duo form, fused)";
+        } else if (P.L == 1 && small && fused) {
+            hipLaunchKernelGGL((k_blind_rotate_duo<1, true, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,
+                               testvec, bk2, out, out_mode, B);
+            if (used) *used = "k_blind_rotate_duo<1,true,true> (duo form, fused)";
+        } else if (P.L == 1 && !small) {
+            hipLaunchKernelGGL((k_blind_rotate_duo<1, false, false>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,
+                               testvec, bk2, out, out_mode, B);
+            if (used) *used = "k_blind_rotate_duo<1,false,false> (duo form)";
+        } else {
+            ok = false;
+        }
+        if (ok) return hipGetLastError();
+        form = 'w';
     }
     if (form == 'p') {  // pair form (2 waves per item); falls back to the whole form where not exact
         bool ok = false;
@@ -3216,7 +3615,8 @@ static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T
                                             const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
                                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (O.br_form) {  // forced form (TFHE_OPT_BR_FORM): the whole batch in one launch
-        const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : O.br_form == 5 ? 'o' : 'w';
+        const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : O.br_form == 5 ? 'o'
+                     : O.br_form == 6 ? 'd' : 'w';
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
     const size_t round = BR_WAVES * device_cus(), tail = B % round;
@@ -3263,7 +3663,7 @@ hipError_t launch_blind_rotate(const KParams &P, const DevTables &T, const uint8
     if (B == 0) return hipSuccess;
     KParams Q = P;
     Q.fallback = 0;
-    const bool fused = small_products(P) && O.arith_strict == 0;
+    const bool fused = small_products(P) && fused_allowed(O);
     if (!fused) Q.tie_flags = nullptr;
     hipError_t e = launch_blind_rotate_forms(Q, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, O, used);
 #ifdef TFHE_FU_UNGUARDED  // A/B builds: the fused arithmetic without its margin guard
@@ -3541,6 +3941,35 @@ __global__ __launch_bounds__(256) void k_checksum(const uint4 *__restrict__ p, s
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+// Largest |x| over a buffer of doubles (the fused arithmetic's key admission,
+// DESIGN.md §6.1): the bit patterns of non-negative doubles order like their
+// values (a NaN above every number), so a 64-bit max per lane, per wave, and
+// one atomic max per wave.
+__global__ __launch_bounds__(256) void k_absmax_f64(const double2 *__restrict__ p, size_t n2, unsigned long long *out) {
+    unsigned long long m = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (size_t)gridDim.x * 256) {
+        const double2 v = p[i];
+        const unsigned long long a = (unsigned long long)__double_as_longlong(v.x) & 0x7FFFFFFFFFFFFFFFull;
+        const unsigned long long b = (unsigned long long)__double_as_longlong(v.y) & 0x7FFFFFFFFFFFFFFFull;
+        m = a > m ? a : m;
+        m = b > m ? b : m;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long x = __shfl_xor(m, o);
+        m = x > m ? x : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+hipError_t launch_absmax(const double *p, size_t count, unsigned long long *out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(*out), s);
+    if (e != hipSuccess || count < 2) return e;
+    const size_t n2 = count / 2;
+    const unsigned blocks = (unsigned)std::min<size_t>((n2 + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_absmax_f64, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const double2 *>(p), n2, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s) {

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "429fac9a75b08927"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "3176deede320ec19"; }

@@ -25,14 +25,15 @@ LIB_PATH = os.environ.get("TFHE_GPU_LIB") or os.path.join(HERE, "lib", "libtfhe_
 OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_groups": 5, "ks_sel_items": 6,
            "circuit_pack": 7, "twiddles": 8, "arith": 9, "br_sync": 10, "br_spin_cap": 11, "host_pipeline": 12,
            "circuit_split": 13}
+READONLY_OPTIONS = {"fused_admitted": 14}  # tfhe_gpu_get_option only
 OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 3, "ks_narrow": 0, "ks_item_groups": 0,
                    "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1, "br_spin_cap": 0,
                    "host_pipeline": 0, "circuit_split": 0}
 # status codes (include/tfhe_gpu.h TFHE_ERR_*)
 ERR_INVALID, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_IO, ERR_DEVICE = -1, -2, -3, -4, -5, -6
-BR_FORMS = {"auto": 0, "whole": 1, "split": 2, "wide": 3, "pair": 4, "octo": 5}
+BR_FORMS = {"auto": 0, "whole": 1, "split": 2, "wide": 3, "pair": 4, "octo": 5, "duo": 6}
 TWIDDLES_GLIBC, TWIDDLES_FDLIBM = 0, 1
-ARITH_AUTO, ARITH_REFERENCE = 0, 1
+ARITH_AUTO, ARITH_REFERENCE, ARITH_FUSED_FORCED = 0, 1, 2
 
 # gate op codes, include/tfhe_gpu.h TFHE_GATE_* (gates.zig:48-121)
 NAND, OR, AND, XOR, XNOR, NOR, ANDNY, ANDYN, ORNY, ORYN = range(10)
@@ -257,11 +258,13 @@ class Context:
         """tfhe_gpu_set_option (kernel forms, twiddle source; OPTIONS)."""
         if name == "br_form" and isinstance(value, str):
             value = BR_FORMS[value]
-        self.check(self.lib.tfhe_gpu_set_option(self.h, OPTIONS[name], int(value)), f"set_option({name})")
+        key = READONLY_OPTIONS[name] if name in READONLY_OPTIONS else OPTIONS[name]  # read-only: the library refuses
+        self.check(self.lib.tfhe_gpu_set_option(self.h, key, int(value)), f"set_option({name})")
 
     def get_option(self, name: str) -> int:
         v = C.c_int64()
-        self.check(self.lib.tfhe_gpu_get_option(self.h, OPTIONS[name], C.byref(v)), f"get_option({name})")
+        key = READONLY_OPTIONS[name] if name in READONLY_OPTIONS else OPTIONS[name]
+        self.check(self.lib.tfhe_gpu_get_option(self.h, key, C.byref(v)), f"get_option({name})")
         return v.value
 
     def reset_options(self):
