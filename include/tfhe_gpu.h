@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 3
+#define TFHE_GPU_ABI_VERSION 4
 
 enum {
     TFHE_OK = 0,
@@ -84,6 +84,8 @@ int         tfhe_gpu_create(const tfhe_params *params, int num_devices, tfhe_gpu
 /* Context on the one HIP device `device` (ABI 2's tfhe_gpu_create). */
 int         tfhe_gpu_create_on_device(const tfhe_params *params, int device, tfhe_gpu_ctx **out);
 void        tfhe_gpu_destroy(tfhe_gpu_ctx *ctx);
+/* Text of the context's last failure; with ctx = NULL, the calling thread's
+ * last failed tfhe_gpu_create / _create_on_device / _create_multi (ABI 4). */
 const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *ctx);
 /* Wait for the context's work; TFHE_ERR_DEVICE if a kernel set the device
  * error word since the last synchronisation.  Every host-buffer entry point
@@ -114,8 +116,20 @@ int         tfhe_gpu_set_stream(tfhe_gpu_ctx *ctx, void *hip_stream);
  * (peer copies over xGMI) before the next (TFHE_OPT_CIRCUIT_SPLIT).  Device-pointer
  * (_dev) and stage entry points and the profile timers use the first device.
  * Nothing is exchanged between devices after the key broadcast. */
+/* Distinct devices must reach each other's memory: create_multi checks
+ * hipDeviceCanAccessPeer for every ordered pair and enables peer access (the
+ * level split's peer copies then go over xGMI, not through the host); a pair
+ * without it fails the create with TFHE_ERR_DEVICE and the pair named in
+ * tfhe_gpu_last_error(NULL).  A device id the node does not have fails with
+ * TFHE_ERR_HIP. */
 int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int *devices, tfhe_gpu_ctx **out);
 int tfhe_gpu_num_devices(const tfhe_gpu_ctx *ctx);
+/* 64-bit fingerprints of the resident device key (BK and KSK in the device
+ * layout; the order-independent k_checksum sum, ~35 us each), the values the
+ * multi-device broadcast compares.  Processes that import a broadcast key
+ * (tfhe_gpu_import_key_device) compare them across ranks (tfhe_dist.py).
+ * TFHE_ERR_NO_KEY without a key.  (ABI 4) */
+int tfhe_gpu_key_fingerprint(tfhe_gpu_ctx *ctx, uint64_t *bk, uint64_t *ksk);
 /* Blind rotations each device of the context has launched since it was
  * created (counts[d] for device d < max_devices, in create order); returns the
  * number of devices.  Shows where a sharded batch or circuit ran. */
@@ -160,10 +174,13 @@ enum {
                                      on devices, or by levels when one component dominates), 1
                                      components, 2 levels (each level's gates split over the devices,
                                      outputs all-gathered by peer copies before the next level) */
-    TFHE_OPT_FUSED_ADMITTED = 14  /* read-only (get_option): 1 if the resident cloud key passed the fused
+    TFHE_OPT_FUSED_ADMITTED = 14, /* read-only (get_option): 1 if the resident cloud key passed the fused
                                      arithmetic's admission check at load (largest BK spectrum component
                                      <= 2^39), 0 if it was refused and TFHE_ARITH_AUTO
                                      runs the reference's expression trees for it */
+    TFHE_OPT_LEVEL_ISSUE_US = 15  /* read-only: host microseconds the last level-split circuit_eval spent
+                                     issuing its per-level launches, peer copies and event waits (one
+                                     host thread for all devices) */
 };
 /* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
  * runs fused multiply-adds in the reference's operation order, with a margin

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 3
+    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 4
 
 
 def test_library_is_gfx950_code_object():
@@ -72,6 +72,7 @@ def test_create_multi_rejects_bad_arguments():
     assert lib.tfhe_gpu_create_multi(C.byref(p), 2, None, C.byref(h)) == -1
     assert not h.value
     assert lib.tfhe_gpu_num_devices(None) == 0
+    assert b"N" in lib.tfhe_gpu_last_error(None)  # ABI 4: the failed create's reason, per thread
 
 
 def test_options_need_a_context():

@@ -65,6 +65,15 @@ class HostCtx:
         ctypes.memmove(self.bk.ctypes.data, bk_ptr, self.bk.nbytes)
         ctypes.memmove(self.ksk.ctypes.data, ksk_ptr, self.ksk.nbytes)
         self.offset, self.tv = offset, np.asarray(tv, np.uint32)
+        if getattr(self, "corrupt_import", False):  # a broken transfer on this rank
+            self.bk[17] ^= 0x40
+
+    def key_fingerprint(self):
+        """Stand-in for tfhe_gpu_key_fingerprint: an order-dependent 64-bit sum of the bytes."""
+        def fp(a):
+            w = np.arange(1, a.size + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+            return int(np.bitwise_xor.reduce(a.astype(np.uint64) * w + w) if a.size else 0)
+        return fp(self.bk), fp(self.ksk)
 
     def gate_batch(self, ops, a, b):
         ops = np.asarray(ops, np.uint32)[:, None]
@@ -100,6 +109,41 @@ def _worker(rank, world, port, q):
         q.put((rank, key_ok, out_ok))
     finally:
         dist.destroy_process_group()
+
+
+def _worker_corrupt(rank, world, port, bad_rank, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = HostCtx(rank)
+        ctx.corrupt_import = rank == bad_rank
+        try:
+            tfhe_dist.broadcast_cloud_key(ctx, "cpu", src=0)
+            q.put((rank, "ok"))
+        except RuntimeError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_key_broadcast_fingerprint_mismatch_fails_every_rank():
+    """A rank whose imported key differs from the source's (a flipped byte in
+    its import) makes broadcast_cloud_key raise on EVERY rank, naming that rank
+    (the cross-rank counterpart of the in-library broadcast's fingerprint check)."""
+    world, bad = 3, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_corrupt, args=(r, world, port, bad, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r for r, _ in res] == list(range(world))
+    for _, msg in res:
+        assert "differs" in msg and f"[{bad}]" in msg, msg
 
 
 @pytest.mark.parametrize("world", [2, 3])

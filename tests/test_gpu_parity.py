@@ -262,6 +262,7 @@ def test_gate_batch_rounds_and_tail(oracle, loader):
     # through pinned staging) gives the same words
     with c.options(br_loader=loader, host_pipeline=1):
         assert np.array_equal(c.gate_batch(ops, A, B), out)
+        assert "k_key_switch_gemm<" in c.last_kernels()  # every chunk: the same key-switch form
 
 
 TRUTH = {0: lambda a, b: ~(a & b), 1: lambda a, b: a | b, 2: lambda a, b: a & b, 3: lambda a, b: a ^ b,
@@ -307,6 +308,37 @@ def test_lut_pbs_uint4(oracle):
                      for t in cts[:4]])
     assert np.array_equal(out[:4], want)
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (msgs + 1) % 16)
+
+
+def test_lut_uint4_on_a_key_with_the_reference_noise_constants(oracle):
+    """the reference draws every KSK with KSK_ALPHA = 2e-5 and
+    every BSK with BSK_ALPHA = 2e-8, the 128-bit constants, for all sets
+    (params.zig:419-422, key.zig:166,202); this build's UINT4 keys use alpha_ksk =
+    alpha_lv0 and alpha_bsk = 0.  A UINT4 cloud key generated by
+    the oracle with the REFERENCE's constants loads and runs: the LUT bootstrap is
+    bit-exact vs the oracle on it.  Decryption is not asserted: with Bg = 2^22 the
+    L = 1 gadget amplifies that BSK noise (the fraction decrypting correctly is
+    printed for the record)."""
+    from oracle import OracleParams, PARAM_SETS
+    p = OracleParams(**dict(PARAM_SETS["uint4"], alpha_ksk=2.0e-5, alpha_bsk=2.0e-8))
+    k0, k1 = oracle.secret_key(p, 42)
+    ck = oracle.cloud_key(p, 43, k0, k1)
+    c = tfhe_amd.Context("uint4", 0)
+    try:
+        c.load_cloud_key(ck.offset, ck.testvec, ck.bk, ck.ksk)
+        m = 16
+        tv = tfhe_amd.lut_generate(c.params, m, lambda x: (x + 1) % m)
+        sk = tfhe_amd.SecretKey(c.params, k0, k1)
+        msgs = np.tile(np.arange(m, dtype=np.uint32), 4)
+        cts = sk.encrypt_lwe_message(msgs, m, seed0=7070)
+        out = c.bootstrap_lut_batch(cts, tv)
+        want = np.array([oracle.gate_batch(p, np.array([255], np.uint8), t[None], t[None], ck, testvec=tv)[0]
+                         for t in cts[:8]])
+        assert np.array_equal(out[:8], want)
+        ok = float(np.mean(sk.decrypt_lwe_message(out, m) == (msgs + 1) % m))
+        print(f"reference-constant UINT4 key: {ok:.2%} of {len(msgs)} LUT outputs decrypt to f(m)")
+    finally:
+        c.close()
 
 
 def test_lut_config5_full_4096_uint4(oracle):

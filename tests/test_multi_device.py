@@ -184,5 +184,63 @@ def test_two_shards_adder_forced_level_split(oracle):
     want, d1 = c.run(single, inputs)
     assert depth == d1 and np.array_equal(got, want)
     assert sum(int(b) << i for i, b in enumerate(sk.decrypt_bool(got[:16]))) == 706
+    # the one host thread's per-level issue for both shards (what an
+    # 8-device level split would pay per level, measured here on two shards)
+    issue_us = multi.get_option("level_issue_us")
+    print(f"level split issue: {issue_us} us for {depth + 1} levels on 2 shards")
+    assert 0 < issue_us
     single.close()
     multi.close()
+
+
+def test_create_multi_distinct_devices(oracle):
+    """Distinct devices: on a one-GPU box, devices = [0, 1] fails cleanly (no
+    crash, no context) with the reason in tfhe_gpu_last_error(NULL); with two or
+    more GPUs the create enables peer access for every pair and the level split
+    and the key broadcast give one device's words (never run on this pool: one
+    GPU per box)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        with pytest.raises(tfhe_amd.TfheError) as e:
+            tfhe_amd.Context.multi("80", devices=[0, 1])
+        assert e.value.status == tfhe_amd.ERR_HIP and "does not exist" in str(e.value)
+        c = tfhe_amd.Context.multi("80", devices=[0, 0])  # the library is still usable
+        c.close()
+        return
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0, 1])
+    assert multi.key_fingerprint() == single.key_fingerprint()
+    sk = tfhe_amd.SecretKey(single.params, k.k0, k.k1)
+    c = tfhe_amd.Circuit()
+    A, Bw = [c.input() for _ in range(16)], [c.input() for _ in range(16)]
+    s, carry = c.ripple_add(A, Bw, c.input())
+    c.output(*s, carry)
+    bits = [(402 >> i) & 1 for i in range(16)] + [(304 >> i) & 1 for i in range(16)] + [0]
+    inputs = sk.encrypt_bool(bits, seed0=808)
+    with multi.options(circuit_split=2):
+        got, _ = c.run(multi, inputs)
+    assert np.array_equal(got, c.run(single, inputs)[0])
+    single.close()
+    multi.close()
+
+
+def test_key_fingerprint(oracle):
+    """tfhe_gpu_key_fingerprint: equal for the same key in two contexts (and on
+    both shards of a two-shard context, which the in-library broadcast checks),
+    different for a key with one BK word changed; no key -> TFHE_ERR_NO_KEY."""
+    a, k = loaded(oracle, "80")
+    b, _ = loaded(oracle, "80", devices=[0, 0])
+    assert a.key_fingerprint() == b.key_fingerprint()
+    bk = np.array(k.ck.bk, copy=True)
+    bk[5, 1, 0, 3] += 1.0
+    c = tfhe_amd.Context("80", 0)
+    c.load_cloud_key(k.ck.offset, k.ck.testvec, bk, k.ck.ksk)
+    fa, fc = a.key_fingerprint(), c.key_fingerprint()
+    assert fa[0] != fc[0] and fa[1] == fc[1]
+    empty = tfhe_amd.Context("80", 0)
+    with pytest.raises(tfhe_amd.TfheError) as e:
+        empty.key_fingerprint()
+    assert e.value.status == tfhe_amd.ERR_NO_KEY
+    for x in (a, b, c, empty):
+        x.close()

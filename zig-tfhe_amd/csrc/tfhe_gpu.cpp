@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>  // types and prototypes only: librccl is dlopen'ed on first multi-device key load
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -127,6 +128,7 @@ struct tfhe_gpu_ctx {
     int64_t twiddle_source = TFHE_TWIDDLES_GLIBC;
     bool key_from_keygen = false;  // the resident BK was transformed with this context's tables
     double bk_absmax = 0.0;        // largest |BK spectrum component| of the resident key, reference scale
+    int64_t level_issue_us = 0;    // host time the last level-split circuit spent issuing (TFHE_OPT_LEVEL_ISSUE_US)
     uint64_t near_tie_items = 0;   // items the margin guard recomputed (device err[1], read by sync_check)
     const char *last_br = "", *last_ks = "";
     std::string last_kernels;
@@ -151,6 +153,13 @@ namespace {
 
 int fail(tfhe_gpu_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
+    return code;
+}
+
+// the calling thread's last failed create (tfhe_gpu_last_error(NULL))
+thread_local std::string g_create_error;
+static int create_fail(int code, const std::string &msg) {
+    g_create_error = msg;
     return code;
 }
 
@@ -516,12 +525,11 @@ int tfhe_gpu_create_on_device(const tfhe_params *params, int device, tfhe_gpu_ct
     if (!out) return TFHE_ERR_INVALID;
     *out = nullptr;
     std::string why;
-    if (!params_ok(params, why)) {
-        std::fprintf(stderr, "tfhe_gpu_create: %s\n", why.c_str());
-        return TFHE_ERR_INVALID;
-    }
+    if (!params_ok(params, why)) return create_fail(TFHE_ERR_INVALID, "tfhe_gpu_create: " + why);
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return TFHE_ERR_HIP;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return create_fail(TFHE_ERR_HIP, "device " + std::to_string(device) + " does not exist (" +
+                                             std::to_string(ndev) + " HIP device(s) visible)");
     auto *c = new tfhe_gpu_ctx();
     c->P = *params;
     c->device = device;
@@ -543,9 +551,9 @@ int tfhe_gpu_create_on_device(const tfhe_params *params, int device, tfhe_gpu_ct
         rc = build_tables(c, TFHE_TWIDDLES_GLIBC);
     } while (0);
     if (rc != TFHE_OK) {
-        std::fprintf(stderr, "tfhe_gpu_create: %s\n", c->err.c_str());
+        const std::string msg = "tfhe_gpu_create: " + c->err;
         tfhe_gpu_destroy(c);
-        return rc;
+        return create_fail(rc, msg);
     }
     *out = c;
     return TFHE_OK;
@@ -573,7 +581,21 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     delete c;
 }
 
-const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *c) { return c ? c->err.c_str() : "null context"; }
+const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *c) {
+    if (c) return c->err.c_str();
+    return g_create_error.empty() ? "null context" : g_create_error.c_str();
+}
+
+int tfhe_gpu_key_fingerprint(tfhe_gpu_ctx *c, uint64_t *bk, uint64_t *ksk) {
+    if (!c || !bk || !ksk) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    uint64_t b = 0, k = 0;
+    const int rc = key_fingerprint(c, b, k);
+    if (rc) return rc;
+    *bk = b;
+    *ksk = k;
+    return TFHE_OK;
+}
 
 int tfhe_gpu_sync(tfhe_gpu_ctx *c) {
     if (!c) return TFHE_ERR_INVALID;
@@ -932,6 +954,20 @@ int pipelined_bootstrap(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, 
     for (hipStream_t &p : c->pipe)
         if (!p) HIPCHK(c, hipStreamCreateWithFlags(&p, hipStreamNonBlocking));
     if (!c->workers) c->workers.reset(new WorkerPool(PIPE_STREAMS));
+    // the GEMM key switch per chunk (the default form where it applies): its MFMA-layout
+    // key is built once on the context stream, and each stream gets its own
+    // partial-sum buffer, so every chunk runs the same key-switch form as the
+    // unpipelined path (last_kernels names it)
+    KsGemm G;
+    rc = ks_gemm_args(c, chunk, G);
+    if (rc) return rc;
+    std::vector<KsGemm> Gs(S, G);
+    if (G.kg) {
+        const size_t pb = ks_gemm_part_bytes(c->K, chunk, 1024, c->K.basebit);
+        rc = ensure(c, c->s_kspart, pb * S);
+        if (rc) return rc;
+        for (int s = 0; s < S; s++) Gs[s].part = (uint32_t *)((char *)c->s_kspart.p + (size_t)s * pb);
+    }
     // everything enqueued on the context stream (key loads, the flags' memset) first
     HIPCHK(c, hipEventRecord(c->pipe_ev, c->stream));
     LaunchOpts o = c->opts;
@@ -969,7 +1005,7 @@ int pipelined_bootstrap(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, 
                                          n, st, o, s == 0 && k == 0 ? &c->last_br : nullptr),
                      "blind rotation") ||
                 !chk(launch_key_switch(c->K, d_lv1 + k0 * 1025, c->d_ksk, d_out + k0 * w, n, st, c->opts,
-                                       s == 0 && k == 0 ? &c->last_ks : nullptr),
+                                       s == 0 && k == 0 ? &c->last_ks : nullptr, &Gs[s]),
                      "key switch") ||
                 !chk(hipMemcpyAsync(c->pin_out + k0 * wb, d_out + k0 * w, n * wb, hipMemcpyDeviceToHost, st), "D2H"))
                 return;
@@ -1724,6 +1760,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_TWIDDLES: *v = c->twiddle_source; break;
     case TFHE_OPT_ARITH: *v = o.arith_strict == 1 ? TFHE_ARITH_REFERENCE : o.arith_strict == 2 ? TFHE_ARITH_FUSED_FORCED : TFHE_ARITH_AUTO; break;
     case TFHE_OPT_FUSED_ADMITTED: *v = o.key_fused_ok; break;
+    case TFHE_OPT_LEVEL_ISSUE_US: *v = c->level_issue_us; break;
     case TFHE_OPT_BR_SYNC: *v = o.br_flags; break;
     case TFHE_OPT_BR_SPIN_CAP: *v = c->K.spin_cap; break;
     case TFHE_OPT_HOST_PIPELINE: *v = c->pipeline; break;
@@ -1998,6 +2035,10 @@ int circuit_eval_levels(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs
         if (rc) rc = fail(c, rc, "device " + std::to_string(s->device) + ": " + s->err);
     }
     size_t ip = 0, op_pos = 0, sp = n_inputs;
+    // the per-level issue (launches, peer copies, event waits) runs on this one
+    // host thread for all devices; it is asynchronous, so it costs wall time only
+    // where it outruns the devices' per-level work (measured: DESIGN.md §7)
+    const auto t_issue = std::chrono::steady_clock::now();
     for (uint32_t lv = 0; lv <= pl.max_level && !rc; lv++) {
         const size_t nb = pl.bs[lv].size(), nn = pl.nots[lv].size(), per = (nb + D - 1) / D;
         if (nb) {
@@ -2043,6 +2084,7 @@ int circuit_eval_levels(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs
             sp += nn;
         }
     }
+    c->level_issue_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_issue).count();
     for (size_t d = 1; d < D && !rc; d++) {  // every device's work done, its error word clean
         tfhe_gpu_ctx *s = c->shards[d];
         if (hipSetDevice(s->device) != hipSuccess) { rc = fail(c, TFHE_ERR_HIP, "hipSetDevice"); break; }
@@ -2169,6 +2211,14 @@ int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int 
     *out = nullptr;
     std::vector<int> devs(num_devices);
     for (int d = 0; d < num_devices; d++) devs[d] = devices ? devices[d] : d;
+    std::string why;
+    if (!params_ok(params, why)) return create_fail(TFHE_ERR_INVALID, "tfhe_gpu_create_multi: " + why);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) return create_fail(TFHE_ERR_HIP, "hipGetDeviceCount failed");
+    for (int d : devs)
+        if (d < 0 || d >= ndev)
+            return create_fail(TFHE_ERR_HIP, "device " + std::to_string(d) + " does not exist (" +
+                                                 std::to_string(ndev) + " HIP device(s) visible)");
     tfhe_gpu_ctx *root = nullptr;
     int rc = tfhe_gpu_create_on_device(params, devs[0], &root);
     if (rc) return rc;
@@ -2185,6 +2235,34 @@ int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int 
     std::vector<int> sorted = devs;
     std::sort(sorted.begin(), sorted.end());
     root->distinct_devices = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (root->distinct_devices) {
+        // every ordered pair: the level split all-gathers between all of them
+        for (int a : devs)
+            for (int b : devs) {
+                if (a == b) continue;
+                int can = 0;
+                hipError_t e = hipDeviceCanAccessPeer(&can, a, b);
+                if (e != hipSuccess || !can) {
+                    tfhe_gpu_destroy(root);
+                    return create_fail(TFHE_ERR_DEVICE, "device " + std::to_string(a) + " cannot access device " +
+                                                            std::to_string(b) + "'s memory (hipDeviceCanAccessPeer" +
+                                                            (e != hipSuccess ? std::string(": ") + hipGetErrorString(e) : "") +
+                                                            "): the multi-device context needs xGMI peer access");
+                }
+                e = hipSetDevice(a);
+                if (e == hipSuccess) e = hipDeviceEnablePeerAccess(b, 0);
+                if (e == hipErrorPeerAccessAlreadyEnabled) {
+                    (void)hipGetLastError();  // clear the sticky status of an already-enabled pair
+                    e = hipSuccess;
+                }
+                if (e != hipSuccess) {
+                    tfhe_gpu_destroy(root);
+                    return create_fail(TFHE_ERR_DEVICE, "hipDeviceEnablePeerAccess(" + std::to_string(a) + " -> " +
+                                                            std::to_string(b) + "): " + hipGetErrorString(e));
+                }
+            }
+        (void)hipSetDevice(devs[0]);
+    }
     *out = root;
     return TFHE_OK;
 }
@@ -2195,9 +2273,12 @@ int tfhe_gpu_create(const tfhe_params *params, int num_devices, tfhe_gpu_ctx **o
     if (!out) return TFHE_ERR_INVALID;
     *out = nullptr;
     std::string why;
-    if (num_devices < 1 || !params_ok(params, why)) return TFHE_ERR_INVALID;
+    if (num_devices < 1 || !params_ok(params, why))
+        return create_fail(TFHE_ERR_INVALID, num_devices < 1 ? "num_devices < 1" : "tfhe_gpu_create: " + why);
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || num_devices > ndev) return TFHE_ERR_HIP;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || num_devices > ndev)
+        return create_fail(TFHE_ERR_HIP, std::to_string(num_devices) + " device(s) requested, " +
+                                             std::to_string(ndev) + " HIP device(s) visible");
     if (num_devices == 1) return tfhe_gpu_create_on_device(params, 0, out);
     return tfhe_gpu_create_multi(params, num_devices, nullptr, out);
 }

@@ -1996,6 +1996,28 @@ DEV void gather_rot1(uint32_t base, int t, int at, uint32_t *xb, uint32_t *v) {
     }
 }
 
+// This wave's share of one level's LDS-DMA: the level slot holds row lo (the
+// a polynomial's row, 16 KB) then row hi (the b polynomial's), 32 pieces of
+// 1 KB; wave w issues pieces w, w + 8 (row lo) and w + 16, w + 24 (row hi),
+// SGPR base + 32-bit lane offset, hand-counted completion (vmcnt).
+DEV void issue_level_share(const double2 *__restrict__ row_lo, const double2 *__restrict__ row_hi, double2 *slot,
+                           int w, int t) {
+    const uint32_t base = (uint32_t)(size_t)(lds_void_t *)slot;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int j = w + 8 * c;
+        const double2 *row = c < 2 ? row_lo : row_hi;
+        const uint32_t voff = (uint32_t)((j & 15) * 1024 + t * 16);
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(base + 1024u * (uint32_t)j);
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(dst), "s"(row)
+            : "memory");
+    }
+}
+
 // One level's whole LDS-DMA by ONE wave (duo form, claimed by the wave that
 // found the slot free first): the level slot holds row lo (the a polynomial's
 // row, 16 KB) then row hi (the b polynomial's), 32 pieces of 1 KB; SGPR base
@@ -2071,6 +2093,14 @@ DEV void mac_row_roles(C2 *po, C2 *px, const C2 *d, const double2 *bk_own, const
     }
 }
 
+#ifndef TFHE_KO_DUO_WAIT  // knock-out timing builds only: every duo-form wait removed (wrong words)
+#define DUO_SPIN(...) spin_until_ge(__VA_ARGS__)
+#else
+#define DUO_SPIN(...) ((void)0)
+#endif
+#ifndef TFHE_DUO_PROTO  // BK slot protocol: 2 = every wave's share after a per-level wait (default), 1 = claims
+#define TFHE_DUO_PROTO 2
+#endif
 #ifndef TFHE_DUO_EX2_REGS  // A/B: 1 = exchange 2 of every transform by permlane / DPP moves (ex2_regs)
 #define TFHE_DUO_EX2_REGS 0
 #endif
@@ -2118,6 +2148,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
 
     auto level_lo = [&](uint32_t k) { return bkd + (size_t)(k / L) * step + (size_t)(k % L) * 1024; };
     auto level_hi = [&](uint32_t k) { return bkd + (size_t)(k / L) * step + (size_t)(L + k % L) * 1024; };
+#if TFHE_DUO_PROTO == 1
     if (w == 0) {  // levels 0 and 1 (claimed: cl = 2) and the zeroed counters
         issue_level_full(level_lo(0), level_hi(0), s_bk, t);
         if (levels > 1) issue_level_full(level_lo(1), level_hi(1), s_bk + 2048, t);
@@ -2129,6 +2160,14 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
             *s_cl = levels > 1 ? 2u : 1u;
         }
     }
+#else
+    // every wave's share of levels 0 and 1; published (8 adds per level) before the
+    // prologue's second barrier
+    if (w == 0 && t < 20) s_sync[t] = 0u;  // pub, done, fwd, hand (bt: written by the h = 0 waves)
+    __syncthreads();
+    issue_level_share(level_lo(0), level_hi(0), s_bk, w, t);
+    if (levels > 1) issue_level_share(level_lo(1), level_hi(1), s_bk + 2048, w, t);
+#endif
     for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
     for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
     if (h == 0) {  // a~_i, b~ (trgsw.zig:297, :312), 64-bit adds
@@ -2139,6 +2178,11 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
             else s_bt[gs] = 2048 - (int)tl;
         }
     }
+#if TFHE_DUO_PROTO != 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    counter_add(s_pub);
+    if (levels > 1) counter_add(s_pub + 1);
+#endif
     __syncthreads();  // tables, a~, b~ and the zeroed counters visible to every wave
     const int bt = __builtin_amdgcn_readfirstlane(s_bt[gs]);
     uint32_t acc[16];  // acc_h = X^{b~} * testvec_h (trgsw.zig:300-306), lane word m = coefficient t + 64m
@@ -2159,6 +2203,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
     const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
     const uint32_t msbs = digit_msbs(L, P.bgbit);
     const uint32_t buf_base = (uint32_t)(size_t)(lds_void_t *)s_buf;  // 4 KB-aligned (BD_LDS_BUF_AT)
+#if TFHE_DUO_PROTO == 1
     // BK levels this wave claimed and has not published yet (at most two: k and k + 1)
     uint32_t owe0 = ~0u, owe1 = ~0u;
     auto publish_owed = [&]() {
@@ -2177,6 +2222,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
         else owe1 = j;
         return true;
     };
+#endif
 
     PhaseProf pp;  // TFHE_PHASE_PROF (tools/phase_prof.hip): per-phase s_memtime per wave
     pp.start();
@@ -2218,6 +2264,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
 #endif
             if (l == L - 1) counter_add(s_fwd + w);  // my exchanges are done: the partner may write my buffer
             pp.mark(2);
+#if TFHE_DUO_PROTO == 1
             // checkpoint: publish the levels I claimed (they had a forward FFT's time to
             // land), then claim levels k and k + 1 if their slots are free and nobody has
             if (owe0 != ~0u) publish_owed();
@@ -2244,6 +2291,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
                     }
                 }
             }
+#else
+            // level k was published at the end of level k - 1 by every wave
+            DUO_SPIN(s_pub + (k & 1), 8u * ((k >> 1) + 1u), fail ? 1u : spin_cap, fail);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             pp.mark(5);
 #ifndef TFHE_KO_MAC
@@ -2252,15 +2303,32 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
 #endif
             __builtin_amdgcn_sched_barrier(0);
             counter_add(s_done + (k & 1));
+#if TFHE_DUO_PROTO != 1
+            pp.mark(3);
+            // end of level k: its slot takes level k + 2 once all 8 waves are through
+            // level k (this wait is the level's one synchronisation), and level k + 1,
+            // issued a level ago, is published
+            if (k + 2 < levels) {
+                DUO_SPIN(s_done + (k & 1), 8u * ((k >> 1) + 1u), fail ? 1u : spin_cap, fail);
+                issue_level_share(level_lo(k + 2), level_hi(k + 2), s_bk + (k & 1) * 2048, w, t);
+                if (k >= 1) {
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                    counter_add(s_pub + ((k + 1) & 1));
+                }
+            } else if (k >= 1 && k + 1 < levels) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                counter_add(s_pub + ((k + 1) & 1));
+            }
+#endif
             pp.mark(1);
         }
         pp.mark(6);
         // hand-off: P_h,(1-h) into the partner's buffer, the partner's into mine
-        spin_until_ge(s_fwd + pw, (uint32_t)i + 1u, fail ? 1u : spin_cap, fail);
+        DUO_SPIN(s_fwd + pw, (uint32_t)i + 1u, fail ? 1u : spin_cap, fail);
 #pragma unroll
         for (int q = 0; q < 8; q++) s_xp[t + 64 * q] = px[q];
         counter_add(s_hand + w);
-        spin_until_ge(s_hand + pw, (uint32_t)i + 1u, fail ? 1u : spin_cap, fail);
+        DUO_SPIN(s_hand + pw, (uint32_t)i + 1u, fail ? 1u : spin_cap, fail);
         __builtin_amdgcn_sched_barrier(0);
         // output h = (rows 0..L-1) + (rows L..2L-1); IEEE addition commutes, so
         // mine + other is that sum for either h

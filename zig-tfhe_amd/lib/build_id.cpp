@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "3176deede320ec19"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "7c526deca9178542"; }

@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("TFHE_GPU_LIB") or os.path.join(HERE, "lib", "libtfhe_
 OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_groups": 5, "ks_sel_items": 6,
            "circuit_pack": 7, "twiddles": 8, "arith": 9, "br_sync": 10, "br_spin_cap": 11, "host_pipeline": 12,
            "circuit_split": 13}
-READONLY_OPTIONS = {"fused_admitted": 14}  # tfhe_gpu_get_option only
+READONLY_OPTIONS = {"fused_admitted": 14, "level_issue_us": 15}  # tfhe_gpu_get_option only
 OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 3, "ks_narrow": 0, "ks_item_groups": 0,
                    "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1, "br_spin_cap": 0,
                    "host_pipeline": 0, "circuit_split": 0}
@@ -100,6 +100,7 @@ _SIGS = {
     "tfhe_gpu_load_cloud_key": (C.c_int, [vp, C.c_uint32, u32p, u32p, f64p, C.c_size_t, u32p, C.c_size_t]),
     "tfhe_gpu_keygen": (C.c_int, [vp, C.c_uint64, C.c_uint64, u32p, u32p, f64p, u32p]),
     "tfhe_gpu_key_blob_bytes": (C.c_int, [vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "tfhe_gpu_key_fingerprint": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "tfhe_gpu_export_key_device": (C.c_int, [vp, vp, vp, u32p, u32p]),
     "tfhe_gpu_import_key_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p]),
     "tfhe_gpu_export_cloud_key": (C.c_int, [vp, C.POINTER(C.c_uint32), u32p, u32p, f64p, u32p]),
@@ -225,8 +226,8 @@ class Context:
             rc = self.lib.tfhe_gpu_create_multi(C.byref(self.params), len(devices), devs, C.byref(h))
             what = "tfhe_gpu_create_multi"
             device = devices[0]
-        if rc != 0:
-            raise TfheError(f"{what} failed ({rc})", rc)
+        if rc != 0:  # tfhe_gpu_last_error(NULL): this thread's last failed create
+            raise TfheError(f"{what} failed ({rc}): {self.lib.tfhe_gpu_last_error(None).decode()}", rc)
         self.h = h
         self.device = device
 
@@ -357,6 +358,12 @@ class Context:
     def key_blob_bytes(self):
         a, b = C.c_size_t(), C.c_size_t()
         self.check(self.lib.tfhe_gpu_key_blob_bytes(self.h, C.byref(a), C.byref(b)), "key_blob_bytes")
+        return a.value, b.value
+
+    def key_fingerprint(self):
+        """tfhe_gpu_key_fingerprint: (bk, ksk) 64-bit sums of the resident device key."""
+        a, b = C.c_uint64(), C.c_uint64()
+        self.check(self.lib.tfhe_gpu_key_fingerprint(self.h, C.byref(a), C.byref(b)), "key_fingerprint")
         return a.value, b.value
 
     def export_key_device(self, bk_dev_ptr: int, ksk_dev_ptr: int):

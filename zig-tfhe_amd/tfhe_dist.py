@@ -56,7 +56,29 @@ def broadcast_cloud_key(ctx, device, src: int = 0, group=None):
         m = meta.cpu().numpy()
         ctx.import_key_device(bk.data_ptr(), ksk.data_ptr(), int(m[0]), m[1:].astype(np.uint32))
     _sync(device)
+    check_key_fingerprints(ctx, device, src, group)
     return bk_bytes + ksk_bytes
+
+
+def check_key_fingerprints(ctx, device, src: int = 0, group=None):
+    """Every rank's resident key must fingerprint like rank `src`'s
+    (tfhe_gpu_key_fingerprint, the same check the in-library multi-device
+    broadcast makes): all-gather the (bk, ksk) sums and raise on any rank whose
+    copy differs, naming it, on EVERY rank (no rank runs gates on a key that
+    some rank holds differently)."""
+    import torch
+    import torch.distributed as dist
+
+    bk_fp, ksk_fp = ctx.key_fingerprint()
+    fdev = "cpu" if dist.get_backend(group) == "gloo" else device  # RCCL needs device tensors
+    mine = torch.tensor([bk_fp - (1 << 63), ksk_fp - (1 << 63)], dtype=torch.int64, device=fdev)  # u64 -> i64
+    parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, mine, group=group)
+    want = parts[src].cpu()
+    bad = [r for r, t in enumerate(parts) if not torch.equal(t.cpu(), want)]
+    if bad:
+        raise RuntimeError(f"cloud-key broadcast: the key on rank(s) {bad} differs from rank {src}'s "
+                           f"(fingerprints {[tuple(int(x) + (1 << 63) for x in t.cpu()) for t in parts]})")
 
 
 def sharded_gate_batch(ctx, ops, a, b, rank: int, world: int, gather: bool = True, group=None):
