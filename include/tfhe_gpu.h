@@ -145,7 +145,9 @@ int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
 enum {
     TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 2 split, 3 latency, 4 pair,
                                      5 octo (8 items per workgroup, two gate waves per SIMD), 6 duo (two
-                                     computing waves per item on one SIMD, no barriers in the step loop) */
+                                     computing waves per item on one SIMD, no barriers in the step loop),
+                                     7 the latency form with split transforms at L = 3 (measured slower,
+                                     DESIGN.md §4.2) */
     TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
     TFHE_OPT_KS_FORM = 3,         /* key switch: 3 auto (default: the one-hot GEMM on the matrix
                                      cores for basebit 2 and 5, else lanes), 0 lanes / ring,

@@ -249,8 +249,10 @@ static int g_fused = 0, g_guard = 0;
  * in fused mode each output's MAC is two fma chains from 0.0, one over the
  * rows of a (0..L-1) and one over the rows of b (L..2L-1), added once at the
  * end, instead of one chain over rows 0..2L-1. */
+/* 2 = "terms" (the latency forms): each row's product is its
+ * own fma chain from 0.0, and the six products are added in row order. */
 static int g_regroup = 0;
-void oracle_set_regroup(int on) { g_regroup = on ? 1 : 0; }
+void oracle_set_regroup(int mode) { g_regroup = mode == 2 ? 2 : mode ? 1 : 0; }
 static __thread int tl_force_ref = 0, tl_near = 0;
 #define FUSED (g_fused && !tl_force_ref)
 void oracle_set_fused(int fused) {
@@ -555,7 +557,21 @@ void oracle_external_product(const oracle_params *p, const double *trgsw_fft,
     double *out_b = (double *)calloc(N, sizeof(double));
     oracle_decomposition(p, trlwe, offset, dec);
     for (uint32_t r = 0; r < R; r++) oracle_ifft(N, dec + (size_t)r * N, dec_fft + (size_t)r * N);
-    if (FUSED && g_regroup) {  /* (rows 0..L-1) + (rows L..2L-1), each chain from 0.0 */
+    if (FUSED && g_regroup == 2) {  /* ((t0 + t1) + t2) + ..., each term from 0.0 */
+        double *ta = (double *)malloc(sizeof(double) * N), *tb = (double *)malloc(sizeof(double) * N);
+        for (uint32_t r = 0; r < R; r++) {
+            const double *row = trgsw_fft + (size_t)r * 2 * N;
+            memset(ta, 0, sizeof(double) * N);
+            memset(tb, 0, sizeof(double) * N);
+            fma_in_fd(N / 2, ta, dec_fft + (size_t)r * N, row);
+            fma_in_fd(N / 2, tb, dec_fft + (size_t)r * N, row + N);
+            for (uint32_t i = 0; i < N; i++) {
+                out_a[i] = r ? out_a[i] + ta[i] : ta[i];
+                out_b[i] = r ? out_b[i] + tb[i] : tb[i];
+            }
+        }
+        free(ta); free(tb);
+    } else if (FUSED && g_regroup) {  /* (rows 0..L-1) + (rows L..2L-1), each chain from 0.0 */
         double *hi_a = (double *)calloc(N, sizeof(double)), *hi_b = (double *)calloc(N, sizeof(double));
         for (uint32_t r = 0; r < R; r++) {
             const double *row = trgsw_fft + (size_t)r * 2 * N;

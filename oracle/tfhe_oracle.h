@@ -145,7 +145,7 @@ double oracle_trig_sin(double x, int source);
 /* 0 = reference expression trees (default); 1 = fused multiply-adds (the
  * MI355X kernels' form at the L=3 / Bg=2^6 sets) */
 void oracle_set_fused(int fused);
-void oracle_set_regroup(int on);  /* fused mode: MAC as (rows of a) + (rows of b), the pair/duo forms */
+void oracle_set_regroup(int mode);  /* fused mode: 1 = (rows of a) + (rows of b) (pair/duo forms), 2 = per-row terms summed (latency forms) */
 int oracle_get_fused(void);
 /* max |x - round(x)| rounded by oracle_fft on this thread since the last call (then reset) */
 double oracle_take_round_error(void);

@@ -114,7 +114,8 @@ def test_key_switch_gemm_full_batches(oracle, B):
 # ---- blind rotation / bootstrap ---------------------------------------------
 @pytest.mark.parametrize("form", ["whole", "whole-noloader", "whole-reference", "whole-noloader-reference",
                                   "whole-barrier", "whole-barrier-reference", "split", "wide", "pair", "pair-reference",
-                                  "octo", "octo-reference", "duo", "duo-reference"])
+                                  "octo", "octo-reference", "duo", "duo-reference", "wide-reference", "wide2",
+                                  "wide2-reference"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
 def test_blind_rotate_vs_oracle(oracle, pname, B, form):
     """All kernel forms (1 wave per item with or without loader waves, fused or
@@ -134,8 +135,10 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
             assert c.last_kernels().startswith("k_blind_rotate_pair<") == (pname == "uint4" or form == "pair")
         if form.startswith("duo"):  # the same rule for the duo form
             assert c.last_kernels().startswith("k_blind_rotate_duo<") == (pname == "uint4" or form == "duo")
-        prefix = {"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<", "wide": "k_blind_rotate_wide<",
-                  "octo": "k_blind_rotate_octo<"}
+        prefix = {"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<", "octo": "k_blind_rotate_octo<",
+                  # wide2 (split transforms) exists at L = 3; UINT4 (L = 1) runs the round-3 latency form
+                  "wide": "k_blind_rotate_wide<",
+                  "wide2": "k_blind_rotate_wide2<" if pname != "uint4" else "k_blind_rotate_wide<"}
         if form.split("-")[0] in prefix:
             assert c.last_kernels().startswith(prefix[form.split("-")[0]])
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
@@ -609,6 +612,9 @@ def test_options_validation_and_report(oracle):
     with c.options(arith=tfhe_amd.ARITH_REFERENCE):
         c.bootstrap_batch(cts)
         assert c.last_kernels() == "k_blind_rotate_wide<3,true,false> (latency form) + " + gemm
+    with c.options(br_form="wide2"):  # the split-transform latency form (round 4, slower), forced
+        c.bootstrap_batch(cts)
+        assert c.last_kernels() == "k_blind_rotate_wide2<3,true,true> (latency form, split transforms, fused) + " + gemm
     with c.options(ks_form=0):
         c.bootstrap_batch(cts)
         assert c.last_kernels().endswith("k_key_switch_lanes<9,2,32,4,1>")

@@ -233,13 +233,13 @@ def _tmp_with_fields(oracle, p, fields):
 def _ext_values(oracle, p, rows, x, mode):
     """Pre-rounding values and words of externalProductWithFft with integer rows
     (2L, 2, N) in `mode` (0 reference trees, 1 fused, 3 fused with the pair / duo
-    forms' regrouped row sums)."""
+    forms' regrouped row sums, 4 fused with the latency forms' summed row terms)."""
     off = oracle.decomposition_offset(p)
     trgsw = np.array([[oracle.ifft((r[0] % (1 << 32)).astype(np.uint32)),
                        oracle.ifft((r[1] % (1 << 32)).astype(np.uint32))] for r in rows])
     try:
-        oracle.set_fused(1 if mode == 3 else mode)
-        oracle.set_regroup(mode == 3)
+        oracle.set_fused(1 if mode in (3, 4) else mode)
+        oracle.set_regroup({3: 1, 4: 2}.get(mode, 0))
         out = {}
         v = oracle.rounded_values(lambda: out.setdefault("w", oracle.external_product(p, trgsw, x, off)))
     finally:
@@ -343,12 +343,13 @@ def test_aligned_adversarial_digits_part_the_trees(oracle):
         near = ((v1 + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0
         assert not (differ & ~near).any()  # every parting coefficient is flagged
         if trial % 4 == 0:
-            v3, w3 = _ext_values(oracle, p, rows, x, 3)
-            delta_rg = max(delta_rg, float(np.abs(v0 - v3).max()))
-            differ3 = w0 != w3
-            part_rg += int(differ3.sum())
-            near3 = ((v3 + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0
-            assert not (differ3 & ~near3).any()
+            for mode in (3, 4):  # the pair / duo forms' regrouped sums; the latency forms' summed terms
+                v3, w3 = _ext_values(oracle, p, rows, x, mode)
+                delta_rg = max(delta_rg, float(np.abs(v0 - v3).max()))
+                differ3 = w0 != w3
+                part_rg += int(differ3.sum())
+                near3 = ((v3 + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0
+                assert not (differ3 & ~near3).any()
     assert mag > 2 ** 47.5
     assert delta < 0.125  # half the guard's 1/4 margin
     assert part > 0
@@ -400,7 +401,7 @@ def test_key_admission_structured_rows(oracle, kind):
         F = [np.where(w * np.sign(rows[i][trial % 2][m]) >= 0, 63, 0) for i in range(6)]
         x = np.concatenate([tmp3(F[0], F[1], F[2]), tmp3(F[3], F[4], F[5])])
         v0, w0 = _ext_values(oracle, p, rows, x, 0)
-        for mode in (1, 3):
+        for mode in (1, 3, 4):
             v, wv = _ext_values(oracle, p, rows, x, mode)
             delta = max(delta, float(np.abs(v0 - v).max()))
             near = ((v + 3377699720527872.5).view(np.uint64) & np.uint64(1)) == 0

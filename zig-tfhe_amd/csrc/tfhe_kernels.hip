@@ -2413,6 +2413,9 @@ DEV void wide_prefetch(double2 (*kr)[2], const double2 *__restrict__ nb, int w, 
 #ifndef WIDE_INV_W0  // A/B: 0 = the round-2 inverse waves 0, 1
 #define WIDE_INV_W0 2
 #endif
+#ifndef WIDE_ROW45_PRIO  // A/B: issue priority of the row waves 4 and 5 (0 = the default, as every wave)
+#define WIDE_ROW45_PRIO 0
+#endif
 #ifndef WIDE_PF_LATE_MASK  // A/B: 0 = every row wave prefetches right after its terms (round-2 schedule)
 #define WIDE_PF_LATE_MASK 0xff
 #endif
@@ -2486,6 +2489,11 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
         for (int m = 0; m < 16; m++) accr[m] = s_acc[ipoly * 1024 + t + 64 * m];
     }
 
+#if WIDE_ROW45_PRIO
+    // rows 4 and 5 share their SIMDs with rows 0 and 1 and finish the forward
+    // phase last; at a higher issue priority they take the VALU first
+    if (w == 4 || w == 5) __builtin_amdgcn_s_setprio(WIDE_ROW45_PRIO);
+#endif
     int at_next = s_at[0];  // a~ read one step ahead (its wait would drain every LDS op)
     uint32_t near = NEAR_NONE;  // FU: margin guard (the inverse waves)
     PhaseProf pp;  // development timing (TFHE_PHASE_PROF), per wave
@@ -2621,6 +2629,344 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
 // candidate words once; each of the G items then picks its word by its
 // wave-uniform digit (readlane -> SGPR), so KSK traffic is per block, not per
 // item.
+// ---------------------------------------------------------------------------
+// Latency form with split transforms (round 4, "wide2"; L = 3): the 6 forward
+// transforms of a step occupy the 4 SIMDs evenly and the 2 inverse transforms
+// all 4, because rows 4 and 5 and both inverse transforms each run as TWO half
+// transforms on two waves of different SIMDs (the round-3
+// form put rows 4 and 5 beside rows 0 and 1 and the inverse on 2 SIMDs).
+// Half h of a 512-point transform holds positions 256h .. 256h + 255 of the
+// bit-reversed DIT array, 4 per lane: stages 1-8 never mix the halves (4 register
+// passes of 2 stages, 3 exchanges through the half's own 4 KB), and stage 9
+// pairs position p with p + 256 through a 4 KB buffer per half and an LDS counter
+// per half.  Every butterfly is the reference's, with its recurrence twiddle,
+// in the same arithmetic as fft512 (the general butterfly equals bf1 / bf_m1 on
+// the exact (1, 0) and (x, -1) twiddles), so the words are the whole form's.
+// Layouts of a half (position bits b0..b7 within it; r = register, t = lane):
+//   P1: r = (b0, b1), t = (b2..b7):           p = r + 4t
+//   P2: r = (b2, b3), t = (b0, b1, b4..b7):   p = (t & 3) + 4r + 16(t >> 2)
+//   P3: r = (b4, b5), t = (b0..b3, b6, b7):   p = (t & 15) + 16r + 64(t >> 4)
+//   P4: r = (b6, b7), t = (b0..b5):           p = t + 64r  (output order)
+// The input of P1 at (t, r) is transform index k = bitrev9(p + 256h) =
+// h + 2 br6(t) + 128 br2(r).  Exchange e stores position p at 16-B slot
+// swz_h<e>(p), an XOR swizzle (searched) under which both its ds_write_b128
+// (P_e) and its ds_read_b128 (P_e+1) are bank-conflict-free.
+// ---------------------------------------------------------------------------
+constexpr uint32_t HSWZ[3][4] = {{0xba, 0xbc, 0x28, 0xe0}, {0x9c, 0xc8, 0x50, 0x50}, {0x88, 0x00, 0xc0, 0x40}};
+template <int E>
+DEV constexpr uint32_t swz_h(uint32_t p) {
+    uint32_t x = 0;
+    for (int i = 0; i < 4; i++) x |= (uint32_t)(__builtin_popcount(p & HSWZ[E][i]) & 1) << i;
+    return p ^ x;
+}
+DEV int br2(int r) { return ((r & 1) << 1) | (r >> 1); }
+DEV uint32_t hp1(int t, int r) { return (uint32_t)(r + 4 * t); }
+DEV uint32_t hp2(int t, int r) { return (uint32_t)((t & 3) + 4 * r + 16 * (t >> 2)); }
+DEV uint32_t hp3(int t, int r) { return (uint32_t)((t & 15) + 16 * r + 64 * (t >> 4)); }
+DEV uint32_t hp4(int t, int r) { return (uint32_t)(t + 64 * r); }
+
+// exchange E of a half: this lane's 4 points at their slots, then the next layout's
+template <int E>
+DEV void half_exchange(C2 *d, C2 *xb, int t) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t p = E == 0 ? hp1(t, r) : E == 1 ? hp2(t, r) : hp3(t, r);
+        xb[swz_h<E>(p)] = d[r];
+    }
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t p = E == 0 ? hp2(t, r) : E == 1 ? hp3(t, r) : hp4(t, r);
+        d[r] = xb[swz_h<E>(p)];
+    }
+    wave_sync();
+}
+
+// Stages 1-8 of half a transform (forward, or INV with the conjugate twiddles).
+// In: P1 with d[r] = point k(t, r); out: P4.  tw = the LDS stage table
+// (index len/2 - 1 + j), a1 = W4[1]'s real part (imaginary part exactly -1).
+template <bool INV, bool FU>
+DEV void half_fft_1to8(C2 *d, C2 *xb, const C2 *tw, double a1, int t) {
+    // pass 1: len 2 (b0), len 4 (b1): the twiddles are lane-uniform, as in passA
+    bf1<FU>(d[0], d[1]);
+    bf1<FU>(d[2], d[3]);
+    bf1<FU>(d[0], d[2]);
+    bf_m1<INV, FU>(d[1], d[3], a1);
+    half_exchange<0>(d, xb, t);
+    {  // pass 2: len 8 (b2 = r bit 0), len 16 (b3 = r bit 1); j0 = b0 + 2 b1 = t & 3
+        const int j0 = t & 3;
+        const C2 w8 = tw[3 + j0], w16a = tw[7 + j0], w16b = tw[7 + j0 + 4];
+        bf<INV, FU>(d[0], d[1], w8);
+        bf<INV, FU>(d[2], d[3], w8);
+        bf<INV, FU>(d[0], d[2], w16a);
+        bf<INV, FU>(d[1], d[3], w16b);
+    }
+    half_exchange<1>(d, xb, t);
+    {  // pass 3: len 32 (b4), len 64 (b5); j0 = b0..b3 = t & 15
+        const int j0 = t & 15;
+        const C2 w32 = tw[15 + j0], w64a = tw[31 + j0], w64b = tw[31 + j0 + 16];
+        bf<INV, FU>(d[0], d[1], w32);
+        bf<INV, FU>(d[2], d[3], w32);
+        bf<INV, FU>(d[0], d[2], w64a);
+        bf<INV, FU>(d[1], d[3], w64b);
+    }
+    half_exchange<2>(d, xb, t);
+    {  // pass 4: len 128 (b6), len 256 (b7); j0 = b0..b5 = t
+        const C2 w128 = tw[63 + t], w256a = tw[127 + t], w256b = tw[127 + t + 64];
+        bf<INV, FU>(d[0], d[1], w128);
+        bf<INV, FU>(d[2], d[3], w128);
+        bf<INV, FU>(d[0], d[2], w256a);
+        bf<INV, FU>(d[1], d[3], w256b);
+    }
+}
+
+// Stage 9 (len 512) across the two halves: position p = t + 64r of half 0 pairs
+// with p + 256 of half 1 (twiddle W512[p]).  Both halves write their P4 points
+// to their own 4 KB (mine), publish a counter, wait for the partner's, and
+// compute the butterfly from (half 0's, half 1's) points: half 0 keeps a, half 1
+// b = 2u - a (it computes a too: the same expression, the same bits).
+template <bool INV, bool FU>
+DEV void half_fft_9(C2 *d, C2 *mine, const C2 *other, uint32_t *cnt_mine, const uint32_t *cnt_other,
+                    uint32_t target, const C2 *tw, int h, int t, uint32_t cap, uint32_t &fail) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) mine[t + 64 * r] = d[r];
+    counter_add(cnt_mine);  // in order after this wave's stores
+    spin_until_ge(cnt_other, target, cap, fail);
+    __builtin_amdgcn_sched_barrier(0);
+    // a uniform branch, not selects (a select of the C2 objects went through scratch)
+    if (h == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            C2 x = other[t + 64 * r];
+            bf<INV, FU>(d[r], x, tw[255 + t + 64 * r]);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            C2 u = other[t + 64 * r];
+            bf<INV, FU>(u, d[r], tw[255 + t + 64 * r]);
+        }
+    }
+}
+
+template <int L, bool SMALL, bool FU = false>
+__global__ __launch_bounds__(512, 1) void k_blind_rotate_wide2(
+    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
+    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
+    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
+    static_assert(L == 3, "split rows 4 and 5: 2L = 6");
+    __shared__ __attribute__((aligned(16))) C2 s_tw[512];
+    __shared__ __attribute__((aligned(16))) C2 s_twist[512];
+    // row r's term spectra (a, b) in s_prod[0/1][r]; s_prod[0][r] is also row r's
+    // exchange buffer (split rows: half h uses its 4 KB); slots 0/1 of s_prod[0]
+    // receive the sums; the inverse halves exchange through s_prod[1][poly]
+    __shared__ __attribute__((aligned(16))) C2 s_prod[2][2 * L][512];
+    __shared__ __attribute__((aligned(16))) C2 s_x9[2][512];  // stage 9: [split row or inverse poly][half]
+    __shared__ __attribute__((aligned(16))) uint32_t s_acc[2048];
+    __shared__ uint16_t s_at[1024];
+    __shared__ uint32_t s_cnt[2][2][2];  // stage-9 counters [forward / inverse][row or poly][half]
+    __shared__ int s_bt;
+    const int tid = threadIdx.x;
+    const int t = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n = P.n;
+    const size_t g = blockIdx.x;
+    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
+    const uint32_t *A = in_a + ia * (size_t)(n + 1);
+    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
+    const int op = ops ? (int)ops[g] : 255;
+    const size_t trgsw = (size_t)2 * L * 1024;  // double2 per BK[i]
+    // roles: waves 0-3 transform rows 0-3 whole and run the inverse halves
+    // (wave 2p + h: polynomial p, half h); waves 4-7 transform rows 4 and 5 in
+    // halves (wave 4 + 2h + s: row 4 + s, half h), one beside each full row on its SIMD
+    const bool full = w < 4;
+    const int hrow = 4 + (w & 1), hh = (w >> 1) & 1;  // split-row role of waves 4-7
+    const int ipoly = w >> 1, ih = w & 1;             // inverse role of waves 0-3
+    const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
+    uint32_t fail = 0;
+
+    for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
+    for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
+    if (tid < 8) (&s_cnt[0][0][0])[tid] = 0u;
+    if (w == 0) {
+        for (int i = t; i <= n; i += 64) {
+            uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
+            uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
+            if (i < n) s_at[i] = (uint16_t)tl;
+            else s_bt = 2048 - (int)tl;
+        }
+    }
+    // BK words of step 0: full rows every frequency t + 64q, split halves q = 4h + r
+    double2 kr[8][2];
+    if (full) {
+        wide_prefetch(kr, bkd, w, t);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int p = 0; p < 2; p++) kr[r][p] = bkd[((size_t)hrow * 8 + 4 * hh + r) * 128 + p * 64 + t];
+    }
+    __syncthreads();
+    const int bt = __builtin_amdgcn_readfirstlane(s_bt);
+    if (w < 2) {
+#pragma unroll
+        for (int m = 0; m < 16; m++) s_acc[w * 1024 + t + 64 * m] = rot_read(testvec + w * 1024, t + 64 * m, bt);
+    }
+    LdsTw T;
+    T.init(s_tw, TT);
+    const C2 *twist_t = s_twist + t;
+    __syncthreads();
+    // inverse halves keep their 8 accumulator words per lane in registers:
+    // coefficients p = 256 ih + t + 64r (r < 4) and p + 512
+    uint32_t accr[8];
+    if (full) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            accr[r] = s_acc[ipoly * 1024 + 256 * ih + t + 64 * r];
+            accr[r + 4] = s_acc[ipoly * 1024 + 512 + 256 * ih + t + 64 * r];
+        }
+    }
+    const uint32_t msbs = digit_msbs(L, P.bgbit);
+    const double a1 = TT.twa[0].x;  // W4[1] = (a1, -1)
+
+    int at_next = s_at[0];
+    uint32_t near = NEAR_NONE;
+    for (int i = 0; i < n; i++) {
+        const int at = __builtin_amdgcn_readfirstlane(at_next);
+        at_next = s_at[i + 1 < n ? i + 1 : i];
+        if (full) {  // row w, whole transform (as k_blind_rotate_wide)
+            const int poly = w >= L ? 1 : 0;
+            const int level = w - poly * L;
+            const uint32_t *pa = s_acc + poly * 1024;
+            uint32_t rot[16], own[16];
+            const int rb = (t - at) & 2047;
+#pragma unroll
+            for (int m = 0; m < 16; m++) {
+                rot[m] = pa[(rb + 64 * m) & 1023];
+                own[m] = pa[t + 64 * m];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            C2 d[1][8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int m = br3(q);
+                const bool n0 = ((rb + 64 * m) & 1024) != 0, n1 = ((rb + 64 * (m + 8)) & 1024) != 0;
+                const uint32_t x0 = ((n0 ? 0u - rot[m] : rot[m]) - own[m] + P.offset) ^ msbs;
+                const uint32_t x1 = ((n1 ? 0u - rot[m + 8] : rot[m + 8]) - own[m + 8] + P.offset) ^ msbs;
+                d[0][q] = twist_in<FU>(digit_f64_flipped(x0, level, P.bgbit), digit_f64_flipped(x1, level, P.bgbit),
+                                       twist_t[64 * m]);
+            }
+            fft512<1, false, FU>(d, s_prod[0][w], T, t);
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                s_prod[0][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][0]);
+                s_prod[1][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][1]);
+            }
+#ifndef TFHE_KO_WIDE_PREFETCH
+            if (i + 1 < n) wide_prefetch(kr, bkd + (size_t)(i + 1) * trgsw, w, t);
+#endif
+        } else {  // row hrow, half hh
+            const uint32_t *pa = s_acc + 1024;  // rows 4, 5: polynomial b, levels 1, 2
+            const int level = hrow - L;
+            const int kb = hh + 2 * br6(t);  // P1 point (t, r) = transform index kb + 128 br2(r)
+            uint32_t rot[8], own[8];
+#pragma unroll
+            for (int m = 0; m < 8; m++) {  // coefficients kb + 128m: k for m < 4, k + 512 for m >= 4
+                const int c = kb + 128 * m;
+                rot[m] = pa[(c - at) & 1023];
+                own[m] = pa[c];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            C2 d[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int m = br2(r), c0 = kb + 128 * m, c1 = c0 + 512;
+                const bool n0 = ((c0 - at) & 1024) != 0, n1 = ((c1 - at) & 1024) != 0;
+                const uint32_t x0 = ((n0 ? 0u - rot[m] : rot[m]) - own[m] + P.offset) ^ msbs;
+                const uint32_t x1 = ((n1 ? 0u - rot[m + 4] : rot[m + 4]) - own[m + 4] + P.offset) ^ msbs;
+                d[r] = twist_in<FU>(digit_f64_flipped(x0, level, P.bgbit), digit_f64_flipped(x1, level, P.bgbit),
+                                    s_twist[c0]);
+            }
+            C2 *xb = &s_prod[0][hrow][256 * hh];
+#ifndef TFHE_KO_FFT
+            half_fft_1to8<false, FU>(d, xb, s_tw, a1, t);
+            half_fft_9<false, FU>(d, &s_x9[hrow - 4][256 * hh], &s_x9[hrow - 4][256 * (1 - hh)],
+                                  &s_cnt[0][hrow - 4][hh], &s_cnt[0][hrow - 4][1 - hh], (uint32_t)i + 1u, s_tw, hh, t,
+                                  fail ? 1u : spin_cap, fail);
+#endif
+            // terms at frequencies f = 256 hh + t + 64r (after this wave's exchanges in xb)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                s_prod[0][hrow][256 * hh + t + 64 * r] = cmul_bk<FU>(d[r], kr[r][0]);
+                s_prod[1][hrow][256 * hh + t + 64 * r] = cmul_bk<FU>(d[r], kr[r][1]);
+            }
+        }
+        __syncthreads();  // every row's terms are in place
+        // sum in the reference's row order 0..2L-1 (fmaInFd1024 starts from 0.0: 0.0 + x == x)
+        const int f = t + 64 * w;
+        C2 fa = s_prod[0][0][f], fb = s_prod[1][0][f];
+#pragma unroll
+        for (int r = 1; r < 2 * L; r++) {
+            const C2 ta = s_prod[0][r][f], tb = s_prod[1][r][f];
+            fa = c2(fa.x + ta.x, fa.y + ta.y);
+            fb = c2(fb.x + tb.x, fb.y + tb.y);
+        }
+        s_prod[0][0][f] = fa;
+        s_prod[0][1][f] = fb;
+        __syncthreads();  // both product spectra complete
+        if (!full) {
+#ifndef TFHE_KO_WIDE_PREFETCH
+            if (i + 1 < n) {  // next step's BK half row, issued in the inverse phase (these waves are idle)
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int p = 0; p < 2; p++)
+                        kr[r][p] = bkd[(size_t)(i + 1) * trgsw + ((size_t)hrow * 8 + 4 * hh + r) * 128 + p * 64 + t];
+            }
+#endif
+        } else {  // inverse half ih of polynomial ipoly
+            const int kb = ih + 2 * br6(t);
+            C2 e[4], twr[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                e[r] = s_prod[0][ipoly][kb + 128 * br2(r)];
+                twr[r] = twist_t[256 * ih + 64 * r];  // untwist of output coefficient 256 ih + t + 64r
+            }
+            C2 *xb = &s_prod[1][ipoly][256 * ih];
+#ifndef TFHE_KO_INV
+            half_fft_1to8<true, FU>(e, xb, s_tw, a1, t);
+            half_fft_9<true, FU>(e, &s_x9[ipoly][256 * ih], &s_x9[ipoly][256 * (1 - ih)], &s_cnt[1][ipoly][ih],
+                                 &s_cnt[1][ipoly][1 - ih], (uint32_t)i + 1u, s_tw, ih, t, fail ? 1u : spin_cap, fail);
+#endif
+            uint32_t *pa = s_acc + ipoly * 1024 + 256 * ih;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                double re, im;
+                untwist_out<false, FU>(e[r], twr[r], re, im);
+                accr[r] += to_torus<SMALL, FU>(re, near);
+                accr[r + 4] += to_torus<SMALL, FU>(im, near);
+                pa[t + 64 * r] = accr[r];
+                pa[t + 64 * r + 512] = accr[r + 4];
+            }
+        }
+        __syncthreads();  // accumulator updated
+    }
+    report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
+    if (FU) near_tie_flag(P, near, g, true);
+
+    if (w != 0) return;
+    if (out_mode == BR_OUT_LV1) {
+        uint32_t *o = out + g * (size_t)1025;
+        for (int j = t; j <= 1024; j += 64) o[j] = j == 0 ? s_acc[0] : j < 1024 ? 0u - s_acc[1024 - j] : s_acc[1024];
+    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {
+        uint32_t *o = out + g * (size_t)(n + 1);
+        for (int j = t; j <= n; j += 64) o[j] = j == 0 ? s_acc[0] : j < n ? 0u - s_acc[n - j] : s_acc[1024];
+    } else {
+        uint32_t *o = out + g * (size_t)2048;
+        for (int j = t; j < 2048; j += 64) o[j] = s_acc[j];
+    }
+}
+
 template <int T, int G>
 __global__ __launch_bounds__(256) void k_key_switch_sel(KParams P, const uint32_t *__restrict__ lv1,
                                                         const uint32_t *__restrict__ ksk,
@@ -3548,7 +3894,17 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     }
 #define BR_LAUNCH(L_, S_)                                                                                         \
     do {                                                                                                          \
-        if (wide && fused) {                                                                                      \
+        if (wide && L_ == 3 && O.br_form == 7) {  /* split transforms (k_blind_rotate_wide2), forced only */     \
+            if (fused) {                                                                                          \
+                hipLaunchKernelGGL((k_blind_rotate_wide2<3, S_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b,   \
+                                   idx, testvec, bk2, out, out_mode, B);                                          \
+                if (used) *used = "k_blind_rotate_wide2<3," #S_ ",true> (latency form, split transforms, fused)"; \
+            } else {                                                                                              \
+                hipLaunchKernelGGL((k_blind_rotate_wide2<3, S_, false>), grid, block, 0, s, P, T, ops, in_a,      \
+                                   in_b, idx, testvec, bk2, out, out_mode, B);                                    \
+                if (used) *used = "k_blind_rotate_wide2<3," #S_ ",false> (latency form, split transforms)";      \
+            }                                                                                                     \
+        } else if (wide && fused) {                                                                               \
             hipLaunchKernelGGL((k_blind_rotate_wide<L_, S_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,  \
                                testvec, bk2, out, out_mode, B);                                                   \
             if (used) *used = "k_blind_rotate_wide<" #L_ "," #S_ ",true> (latency form, fused)";                  \
@@ -3683,8 +4039,8 @@ static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T
                                             const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
                                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (O.br_form) {  // forced form (TFHE_OPT_BR_FORM): the whole batch in one launch
-        const char f = O.br_form == 2 ? 's' : O.br_form == 3 ? 'W' : O.br_form == 4 ? 'p' : O.br_form == 5 ? 'o'
-                     : O.br_form == 6 ? 'd' : 'w';
+        const char f = O.br_form == 2 ? 's' : O.br_form == 3 || O.br_form == 7 ? 'W' : O.br_form == 4 ? 'p'
+                     : O.br_form == 5 ? 'o' : O.br_form == 6 ? 'd' : 'w';
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
     const size_t round = BR_WAVES * device_cus(), tail = B % round;
