@@ -394,6 +394,21 @@ DEV void ex2_read(C2 *d, const C2 *xb, int t) {
 // ONEBUF: both transforms exchange through one 8 KB buffer.  Every write
 // into it follows, in this wave's program order, the reads of the data it
 // overwrites, and one wave's LDS operations execute in order.
+// TFHE_X2_WAITS (A/B): one explicit lgkmcnt wait per read group instead of
+// hipcc's one per consumed read (a single wave issues every s_waitcnt too).
+// lgkmcnt(n): the LDS unit completes a wave's operations in order, so waiting
+// until n remain leaves exactly the n youngest (a group of writes) in flight.
+#ifndef TFHE_X2_WAITS
+#define TFHE_X2_WAITS 0
+#endif
+#define X2_LGKM(n_)                                                                 \
+    do {                                                                            \
+        if (TFHE_X2_WAITS) {                                                        \
+            __builtin_amdgcn_sched_barrier(0);                                      \
+            __builtin_amdgcn_s_waitcnt(0xC07F | ((n_) << 8));                        \
+            __builtin_amdgcn_sched_barrier(0);                                      \
+        }                                                                           \
+    } while (0)
 template <bool INV, bool ONEBUF = false, bool FU = false, class TW>
 DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     C2 *x0 = xb, *x1 = ONEBUF ? xb : xb + 512;
@@ -406,6 +421,7 @@ DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     ex1_write(d[1], x1, t);
     wave_sync();
     T.pass_b(wb_, t);
+    X2_LGKM(0);
     passBC<INV, FU>(d[0], wb_);
     ex1_read(d[1], x1, t);
 #ifdef TFHE_EX2_REGS_X2  // register exchange 2 here too: 7.75 vs 7.52 ms per 1,024 gates (not kept)
@@ -419,14 +435,17 @@ DEV void fft512_x2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
 #else
     ex2_write(d[0], x0, t);
     wave_sync();
+    X2_LGKM(8);
     passBC<INV, FU>(d[1], wb_);
     T.pass_c(wc_, t);
     ex2_read(d[0], x0, t);
     ex2_write(d[1], x1, t);
     wave_sync();
+    X2_LGKM(8);
     passBC<INV, FU>(d[0], wc_);
     ex2_read(d[1], x1, t);
     wave_sync();
+    X2_LGKM(0);
     passBC<INV, FU>(d[1], wc_);
 #endif
 }
@@ -963,6 +982,29 @@ DEV void load_digits_pair0_regs(C2 (*d)[8], const uint32_t *tA, const uint32_t *
     }
 }
 
+// Digits of rows (2rp, 2rp+1), rp = 1, 2 at L = 3, from packed tmp words kept in
+// registers (round 4): tbx[m] = tmp_b's word m with tmp_a's level-2 field moved
+// into its unused low bits (tmp_b's fields sit at bits >= 32 - 3 bgbit > bgbit).
+// Row 2 (a, level 2) reads bits [0, bgbit), rows 3-5 (b, levels 0-2) their own
+// fields: one v_bfe_i32 per digit as before, and no tmp round trip through LDS
+// (32 ds_write_b32 + 48 ds_read_b32 per step fewer).
+template <bool FU>
+DEV void load_digits_pair_tbx(C2 (*d)[8], const uint32_t *tbx, int rp, int bgbit, const C2 *twist_t) {
+    const int off0 = rp == 1 ? 0 : 32 - 2 * bgbit, off1 = rp == 1 ? 32 - bgbit : 32 - 3 * bgbit;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int m = br3(q);
+        const C2 w = twist_t[64 * m];
+        d[0][q] = twist_in<FU>((double)(int32_t)__builtin_amdgcn_sbfe(tbx[m], off0, bgbit),
+                               (double)(int32_t)__builtin_amdgcn_sbfe(tbx[m + 8], off0, bgbit), w);
+        d[1][q] = twist_in<FU>((double)(int32_t)__builtin_amdgcn_sbfe(tbx[m], off1, bgbit),
+                               (double)(int32_t)__builtin_amdgcn_sbfe(tbx[m + 8], off1, bgbit), w);
+    }
+}
+#ifndef TFHE_TMP_LDS  // A/B: 1 = the round-3 tmp words staged through LDS for row pairs 1 and 2
+#define TFHE_TMP_LDS 0
+#endif
+
 // Row pairs of one CMUX step: forward FFTs of rows (2rp, 2rp+1), wait for the
 // pair's BK rows in LDS, MAC, release the buffer and prefetch the next pair.
 // LDS-DMA of one BK row pair (32 KB) into a slot, 8 x 16 B per thread, in
@@ -987,7 +1029,8 @@ template <int L, bool LOADER, bool FU = false, bool FLAGS = false>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
                   PhaseProf &pp, uint32_t &fail, uint32_t spin_cap, uint32_t *sync = nullptr, uint32_t k0 = 0,
-                  const uint32_t *tA = nullptr, const uint32_t *tB = nullptr, const C2 *tw0 = nullptr) {
+                  const uint32_t *tA = nullptr, const uint32_t *tB = nullptr, const C2 *tw0 = nullptr,
+                  const uint32_t *tbx = nullptr) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // fmaInFd1024 accumulates from 0.0 (0.0 + x == x)
         fa[q] = c2(0.0, 0.0);
@@ -1014,6 +1057,9 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
             load_digits_pair0_regs<FU>(d, tA, tB, L, bgbit, tw0);
         else
 #endif
+        if (!TFHE_TMP_LDS && PAIR_UNROLL == L && LOADER && L == 3)
+            load_digits_pair_tbx<FU>(d, tbx, rp, bgbit, twist_t);
+        else
             load_digits_pair_lds<FU>(d, s_tmp, 2 * rp, L, bgbit, twist_t, t);
 #ifndef TFHE_KO_FFT  // TFHE_KO_*: development knock-out builds (timing only)
         fft512_x2<false, true, FU>(d, xb, T, t);
@@ -1193,6 +1239,9 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
     const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
     const uint32_t msbs = digit_msbs(L, P.bgbit);
     const uint32_t acc_base = (uint32_t)(size_t)(lds_void_t *)s_acc;  // 4 KB-aligned (BR_LDS_ACC_AT)
+    // tmp words stay in registers for every row pair (load_digits_pair_tbx): the loader
+    // form at L = 3 (its unrolled pair loop), unless TFHE_TMP_LDS
+    constexpr bool tmp_regs = !TFHE_TMP_LDS && LOADER && L == 3;
 
     for (int i = 0; i < n; i++) {
         pp.mark(0);
@@ -1201,7 +1250,7 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         const int at = __builtin_amdgcn_readfirstlane(at_next);
         // tmp = X^{a~} acc - acc (+ decomposition offset), written over the
         // accumulator's LDS copy (the old acc stays in accA/accB registers)
-        uint32_t tA[16], tB[16];
+        uint32_t tA[16], tB[16], tbx[16];
         C2 tw0[8];
 #ifndef TFHE_KO_TMP
         // all 32 gathers first (one wait), then the arithmetic: interleaved,
@@ -1222,6 +1271,11 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
             tA[m] = tmp_word(tA[m], sg, off_s, accA[m], msbs);
             tB[m] = tmp_word(tB[m], sg, off_s, accB[m], msbs);
         }
+        if constexpr (tmp_regs) {  // pairs 1, 2 read tbx (load_digits_pair_tbx), not LDS
+#pragma unroll
+            for (int m = 0; m < 16; m++)
+                tbx[m] = __builtin_amdgcn_ubfe(tA[m], 32 - L * P.bgbit, P.bgbit) | (tB[m] & ~((1u << P.bgbit) - 1u));
+        }
 #else
 #pragma unroll
         for (int m = 0; m < 16; m++) {
@@ -1229,18 +1283,20 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
             tB[m] = accB[m] * at + P.offset;
         }
 #endif
-        wave_sync();
+        if constexpr (!tmp_regs) {
+            wave_sync();
 #pragma unroll
-        for (int m = 0; m < 16; m++) {
-            s_acc[t + 64 * m] = tA[m];
-            s_acc[1024 + t + 64 * m] = tB[m];
+            for (int m = 0; m < 16; m++) {
+                s_acc[t + 64 * m] = tA[m];
+                s_acc[1024 + t + 64 * m] = tB[m];
+            }
+            wave_sync();
         }
-        wave_sync();
         C2 fa[8], fb[8];
         at_next = s_at[i + 1 < n ? i + 1 : i];
         br_pairs<L, LOADER, FU, FLAGS>(s_acc, P.bgbit, T, twist_t, s_x, t, tid, fa, fb, s_bk, (L * i) & 1,
                                        bkd + (size_t)i * step_stride + 2048, i + 1 < n, pp, fail, spin_cap, s_sync,
-                                       (uint32_t)(L * i), tA, tB, tw0);
+                                       (uint32_t)(L * i), tA, tB, tw0, tbx);
         pp.mark(5);
         inverse_and_add<SMALL, 64, true, FU>(fa, fb, s_x, T, twist_t, t, accA, accB, near);
         wave_sync();
@@ -2414,7 +2470,7 @@ DEV void wide_prefetch(double2 (*kr)[2], const double2 *__restrict__ nb, int w, 
 #define WIDE_INV_W0 2
 #endif
 #ifndef WIDE_ROW45_PRIO  // A/B: issue priority of the row waves 4 and 5 (0 = the default, as every wave)
-#define WIDE_ROW45_PRIO 0
+#define WIDE_ROW45_PRIO 1
 #endif
 #ifndef WIDE_PF_LATE_MASK  // A/B: 0 = every row wave prefetches right after its terms (round-2 schedule)
 #define WIDE_PF_LATE_MASK 0xff

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "401bf4ef5abd48e7"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "4e48b30123fddc13"; }
