@@ -7,7 +7,7 @@
 #include <cstdio>
 
 template <int OP, int C>
-__device__ __forceinline__ void body(double (&a)[16], const double (&b)[16], unsigned (&u)[16]) {
+__device__ __forceinline__ void body(double (&a)[16], const double (&b)[16], unsigned (&u)[16], double sc) {
 #pragma unroll
     for (int i = 0; i < C; i++) {
         if constexpr (OP == 0) asm volatile("v_add_f64 %0, %0, %1" : "+v"(a[i]) : "v"(b[i]));
@@ -19,12 +19,20 @@ __device__ __forceinline__ void body(double (&a)[16], const double (&b)[16], uns
             asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 15]));
         }
         if constexpr (OP == 5) asm volatile("v_trunc_f64 %0, %0" : "+v"(a[i]));
+        if constexpr (OP == 6) asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(a[i]) : "v"(b[i]), "v"(b[(i + 1) & 15]));
+        if constexpr (OP == 7) asm volatile("v_fmac_f64 %0, %1, %2" : "+v"(a[i]) : "v"(b[i]), "v"(b[(i + 1) & 15]));
+        if constexpr (OP == 8) asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(a[i]) : "v"(b[i]));
+        if constexpr (OP == 9) {  // fma with a lane-uniform (SGPR) multiplier, as the pass-A twiddles
+            asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(a[i]) : "v"(b[i]), "s"(sc));
+        }
+        if constexpr (OP == 10) asm volatile("v_add_f64 %0, %0, %1" : "+v"(a[i]) : "s"(sc));
     }
 }
-static const char *NAMES[] = {"v_add_f64", "v_mul_f64", "v_add_u32", "v_cvt_f64_i32", "add_f64+add_u32", "v_trunc_f64"};
+static const char *NAMES[] = {"v_add_f64", "v_mul_f64", "v_add_u32", "v_cvt_f64_i32", "add_f64+add_u32", "v_trunc_f64",
+                              "v_fma_f64", "v_fmac_f64", "v_fma_f64 a*a+c", "v_fma_f64 sgpr", "v_add_f64 sgpr"};
 
 template <int OP, int C>
-__global__ void k_rate(double *out, int iters) {
+__global__ void k_rate(double *out, int iters, double sc) {
     double a[16], b[16];
     unsigned u[16];
     for (int i = 0; i < 16; i++) {
@@ -33,10 +41,10 @@ __global__ void k_rate(double *out, int iters) {
         u[i] = threadIdx.x + i;
     }
     for (int k = 0; k < iters; k++) {
-        body<OP, C>(a, b, u);
-        body<OP, C>(a, b, u);
-        body<OP, C>(a, b, u);
-        body<OP, C>(a, b, u);
+        body<OP, C>(a, b, u, sc);
+        body<OP, C>(a, b, u, sc);
+        body<OP, C>(a, b, u, sc);
+        body<OP, C>(a, b, u, sc);
     }
     double s = 0;
     for (int i = 0; i < 16; i++) s += a[i] + u[i];
@@ -46,14 +54,14 @@ __global__ void k_rate(double *out, int iters) {
 template <int OP, int C>
 void run(double *out, int wps) {
     const int iters = 16000 / C, blocks = 256, threads = 256 * wps;
-    hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, 10);
+    hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, 10, 1.0000001);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     float best = 1e9;
     for (int r = 0; r < 3; r++) {
         hipEventRecord(e0);
-        hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, iters);
+        hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, iters, 1.0000001);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
@@ -84,6 +92,11 @@ int main() {
     run_op<3>(out);
     run_op<4>(out);
     run_op<5>(out);
+    run_op<6>(out);
+    run_op<7>(out);
+    run_op<8>(out);
+    run_op<9>(out);
+    run_op<10>(out);
     hipDeviceSynchronize();
     return 0;
 }
