@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "4e48b30123fddc13"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "94fc3d60340ab112"; }
