@@ -1068,7 +1068,9 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
         const int slot = (slot0 + rp) & 1;
         if (FLAGS) {  // pair k = k0 + rp is use (k >> 1) of slot k & 1: wait until all 4 loaders published it
             const uint32_t k = k0 + (uint32_t)rp;
+#ifndef TFHE_KO_WAIT  // knock-out timing build: no wait for the pair's publication (wrong words possible)
             spin_until_ge(sync + (k & 1), 4u * ((k >> 1) + 1u), spin_cap, fail);
+#endif
             __builtin_amdgcn_sched_barrier(0);  // as the barrier did: nothing moves across the wait
         } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the pair's DMA landed
@@ -2154,12 +2156,59 @@ DEV void mac_row_roles(C2 *po, C2 *px, const C2 *d, const double2 *bk_own, const
 #else
 #define DUO_SPIN(...) ((void)0)
 #endif
-#ifndef TFHE_DUO_PROTO  // BK slot protocol: 2 = every wave's share after a per-level wait (default), 1 = claims
-#define TFHE_DUO_PROTO 2
+#ifndef TFHE_DUO_PROTO  // BK protocol: 2 = LDS slots, every wave's share after a per-level wait (default),
+#define TFHE_DUO_PROTO 2  // 1 = LDS slots by claims, 3 = no LDS slots: each wave loads its row from L2 into registers
 #endif
+
+// Duo protocol 3: wave h's BK row for level k (row hL + k % L of BK[k / L]),
+// parts [q][a|b][lane]: kr[q][0] = frequency t + 64q of output part h (own),
+// kr[q][1] of part 1 - h (the partner's); 16 x 16 B per lane, coalesced 1 KB
+// per wave-instruction, landing under the next forward transform (the 4 items
+// of a workgroup read the same row: L1/L2 hits)
+// (wave-uniform piece bases in SGPRs, one shared 32-bit lane offset: hipcc
+// otherwise hoists 16 64-bit per-lane addresses out of the step loop and spills)
+DEV const double2 *sgpr_ptr(const double2 *p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const double2 *>(((uint64_t)hi << 32) | lo);
+}
+DEV void duo_row_load(double2 (*kr)[2], const double2 *__restrict__ row, int h, int t) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        kr[q][0] = sgpr_ptr(row + (2 * q + h) * 64)[t];
+        kr[q][1] = sgpr_ptr(row + (2 * q + 1 - h) * 64)[t];
+    }
+}
+template <bool FU>
+DEV void mac_row_regs(C2 *po, C2 *px, const C2 *d, const double2 (*kr)[2]) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const C2 x = d[q];
+        const double2 ko = kr[q][0], kx = kr[q][1];
+        if (FU) {
+            po[q] = c2(fmad(x.x, ko.x, fmad(-x.y, ko.y, po[q].x)), fmad(x.x, ko.y, fmad(x.y, ko.x, po[q].y)));
+            px[q] = c2(fmad(x.x, kx.x, fmad(-x.y, kx.y, px[q].x)), fmad(x.x, kx.y, fmad(x.y, kx.x, px[q].y)));
+        } else {
+            const C2 to = c2(x.x * ko.x - x.y * ko.y, x.x * ko.y + x.y * ko.x);
+            const C2 tx = c2(x.x * kx.x - x.y * kx.y, x.x * kx.y + x.y * kx.x);
+            po[q] = c2(po[q].x + to.x, po[q].y + to.y);
+            px[q] = c2(px[q].x + tx.x, px[q].y + tx.y);
+        }
+    }
+}
 #ifndef TFHE_DUO_EX2_REGS  // A/B: 1 = exchange 2 of every transform by permlane / DPP moves (ex2_regs)
 #define TFHE_DUO_EX2_REGS 0
 #endif
+
+// Protocol 3: the lane index as a value hipcc cannot hoist out of the step
+// loop, so the transforms' swizzled exchange addresses are computed where they
+// are used instead of living (and spilling) beside the prefetched BK row.
+DEV int duo_lane(int t) {
+#if TFHE_DUO_PROTO == 3
+    asm volatile("" : "+v"(t));
+#endif
+    return t;
+}
 
 template <int L, bool SMALL, bool FU>
 __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
@@ -2216,6 +2265,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
             *s_cl = levels > 1 ? 2u : 1u;
         }
     }
+#elif TFHE_DUO_PROTO == 3
+    if (w == 0 && t < 20) s_sync[t] = 0u;  // fwd, hand (pub, done unused)
+    double2 kr[8][2];
+    duo_row_load(kr, bkd + (size_t)h * L * 1024, h, t);  // level 0: row hL of BK[0]
 #else
     // every wave's share of levels 0 and 1; published (8 adds per level) before the
     // prologue's second barrier
@@ -2234,18 +2287,24 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
             else s_bt[gs] = 2048 - (int)tl;
         }
     }
-#if TFHE_DUO_PROTO != 1
+#if TFHE_DUO_PROTO == 2
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     counter_add(s_pub);
     if (levels > 1) counter_add(s_pub + 1);
 #endif
     __syncthreads();  // tables, a~, b~ and the zeroed counters visible to every wave
     const int bt = __builtin_amdgcn_readfirstlane(s_bt[gs]);
+    // protocol 3 keeps no BK in LDS: the former slots hold each wave's accumulator
+    // (4 KB-aligned), and acc lives in registers only from the hand-off to the
+    // step's end (the prefetched BK row takes its registers during the forward phase)
+    constexpr bool ACC_LDS = TFHE_DUO_PROTO == 3;
+    uint32_t *s_acc = ACC_LDS ? reinterpret_cast<uint32_t *>(smem) + w * 1024 : s_buf;
+    uint32_t *s_tmpw = reinterpret_cast<uint32_t *>(smem) + (8 + w) * 1024;  // protocol 3: tmp words too
     uint32_t acc[16];  // acc_h = X^{b~} * testvec_h (trgsw.zig:300-306), lane word m = coefficient t + 64m
 #pragma unroll
     for (int m = 0; m < 16; m++) {
         acc[m] = rot_read(testvec + h * 1024, t + 64 * m, bt);
-        s_buf[t + 64 * m] = acc[m];
+        s_acc[t + 64 * m] = acc[m];
     }
     wave_sync();
     LdsTwAtPass T;
@@ -2258,7 +2317,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
     // error word), every later wait polls once: a broken protocol ends fast
     const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
     const uint32_t msbs = digit_msbs(L, P.bgbit);
-    const uint32_t buf_base = (uint32_t)(size_t)(lds_void_t *)s_buf;  // 4 KB-aligned (BD_LDS_BUF_AT)
+    const uint32_t buf_base = (uint32_t)(size_t)(lds_void_t *)s_acc;  // 4 KB-aligned (BD_LDS_BUF_AT; smem)
 #if TFHE_DUO_PROTO == 1
     // BK levels this wave claimed and has not published yet (at most two: k and k + 1)
     uint32_t owe0 = ~0u, owe1 = ~0u;
@@ -2289,11 +2348,19 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
         // tmp_h = X^{a~} acc_h - acc_h + offset (flipped digit fields), in registers
         uint32_t tmp[16], xb[16];
         gather_rot1(buf_base, t, at, xb, tmp);
+        if (ACC_LDS) {
+#pragma unroll
+            for (int m = 0; m < 16; m++) acc[m] = s_acc[t + 64 * m];
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 0; m < 16; m++) {
             const uint32_t sg = gather_sign(xb[m]), off_s = P.offset - sg;
             tmp[m] = tmp_word(tmp[m], sg, off_s, acc[m], msbs);
+        }
+        if (ACC_LDS) {
+#pragma unroll
+            for (int m = 0; m < 16; m++) s_tmpw[t + 64 * m] = tmp[m];
         }
         wave_sync();  // the gather's reads precede the exchanges' writes into the buffer
         // partial sums over this wave's rows: po for output h (kept), px for
@@ -2309,6 +2376,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
         for (int l = 0; l < L; l++) {
             const uint32_t k = (uint32_t)(L * i + l);  // level k of the launch lives in slot k & 1
             C2 d[1][8];
+            if (ACC_LDS) {
+#pragma unroll
+                for (int m = 0; m < 16; m++) tmp[m] = s_tmpw[t + 64 * m];
+            }
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 const int m = br3(q);
@@ -2316,7 +2387,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
                                        twist_t[64 * m]);
             }
 #ifndef TFHE_KO_FFT
-            fft512<1, false, FU, LdsTwAtPass, EX2LDS>(d, s_x, T, t);
+            fft512<1, false, FU, LdsTwAtPass, EX2LDS>(d, s_x, T, duo_lane(t));
 #endif
             if (l == L - 1) counter_add(s_fwd + w);  // my exchanges are done: the partner may write my buffer
             pp.mark(2);
@@ -2347,19 +2418,29 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
                     }
                 }
             }
-#else
+#elif TFHE_DUO_PROTO == 2
             // level k was published at the end of level k - 1 by every wave
             DUO_SPIN(s_pub + (k & 1), 8u * ((k >> 1) + 1u), fail ? 1u : spin_cap, fail);
 #endif
             __builtin_amdgcn_sched_barrier(0);
             pp.mark(5);
+#if TFHE_DUO_PROTO == 3
+#ifndef TFHE_KO_MAC
+            mac_row_regs<FU>(po, px, d[0], kr);
+#endif
+#ifndef TFHE_KO_DUO_LOAD  // knock-out timing build: the prologue's row reused (wrong words)
+            if (k + 1 < levels)  // the next level's row, under the next transform (or the inverse)
+                duo_row_load(kr, bkd + (size_t)((k + 1) / L) * step + (size_t)(h * L + (k + 1) % L) * 1024, h, t);
+#endif
+#else
 #ifndef TFHE_KO_MAC
             // row hL + l, parts [q][a|b][lane]: output h's part at +64h, the other's at +64(1-h)
             mac_row_roles<FU>(po, px, d[0], s_bk + (k & 1) * 2048 + h * 1024 + 64 * h, s_bk + (k & 1) * 2048 + h * 1024 + 64 * (1 - h), t);
 #endif
             __builtin_amdgcn_sched_barrier(0);
             counter_add(s_done + (k & 1));
-#if TFHE_DUO_PROTO != 1
+#endif
+#if TFHE_DUO_PROTO == 2
             pp.mark(3);
             // end of level k: its slot takes level k + 2 once all 8 waves are through
             // level k (this wait is the level's one synchronisation), and level k + 1,
@@ -2396,10 +2477,14 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
             const C2 mine = po[m];
             e[0][q] = c2(mine.x + o.x, mine.y + o.y);
         }
+        if (ACC_LDS) {  // back into registers for the update, landing under the inverse transform
+#pragma unroll
+            for (int m = 0; m < 16; m++) acc[m] = s_acc[t + 64 * m];
+        }
         wave_sync();  // the partial's reads precede the inverse's exchange writes
         pp.mark(7);
 #ifndef TFHE_KO_INV
-        fft512<1, true, FU, LdsTwAtPass, EX2LDS>(e, s_x, T, t);
+        fft512<1, true, FU, LdsTwAtPass, EX2LDS>(e, s_x, T, duo_lane(t));
 #endif
         uint32_t nq[2] = {NEAR_NONE, NEAR_NONE};
 #pragma unroll
@@ -2412,7 +2497,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
         near &= nq[0] & nq[1];
         wave_sync();
 #pragma unroll
-        for (int m = 0; m < 16; m++) s_buf[t + 64 * m] = acc[m];
+        for (int m = 0; m < 16; m++) s_acc[t + 64 * m] = acc[m];
         wave_sync();
     }
     pp.mark(0);
@@ -2427,20 +2512,20 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
     if (out_mode == BR_OUT_LV1) {  // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
         uint32_t *o = out + g * (size_t)1025;
         if (h == 0) {
-            for (int j = t; j < 1024; j += 64) o[j] = j == 0 ? s_buf[0] : 0u - s_buf[1024 - j];
+            for (int j = t; j < 1024; j += 64) o[j] = j == 0 ? s_acc[0] : 0u - s_acc[1024 - j];
         } else if (t == 0) {
-            o[1024] = s_buf[0];
+            o[1024] = s_acc[0];
         }
     } else if (out_mode == BR_OUT_LV0_EXTRACT2) {  // sampleExtractIndex2 (trlwe.zig:165-180)
         uint32_t *o = out + g * (size_t)(n + 1);
         if (h == 0) {
-            for (int j = t; j < n; j += 64) o[j] = j == 0 ? s_buf[0] : 0u - s_buf[n - j];
+            for (int j = t; j < n; j += 64) o[j] = j == 0 ? s_acc[0] : 0u - s_acc[n - j];
         } else if (t == 0) {
-            o[n] = s_buf[0];
+            o[n] = s_acc[0];
         }
     } else {
         uint32_t *o = out + g * (size_t)2048 + h * 1024;
-        for (int j = t; j < 1024; j += 64) o[j] = s_buf[j];
+        for (int j = t; j < 1024; j += 64) o[j] = s_acc[j];
     }
 }
 
