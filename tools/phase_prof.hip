@@ -1,5 +1,7 @@
 // Development tool: per-phase s_memtime breakdown of the blind-rotation kernel
 // on a 1024-gate 128-bit batch with random operands (timing only, no parity).
+//   (-DTFHE_SPIN_STATS instead of -DTFHE_PHASE_PROF: no phase marks, only the count of
+//   slot-wait polls that found the pair unpublished, i.e. slept)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DTFHE_PHASE_PROF \
 //         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
 #define TFHE_SINGLE_TU
@@ -43,7 +45,12 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int rep = 0; rep < 2; rep++) {
         unsigned long long z[128] = {0};
+#ifdef TFHE_PHASE_PROF
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
+#endif
+#ifdef TFHE_SPIN_STATS
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_stats), z, 4 * sizeof(unsigned long long)));
+#endif
         CK(hipEventRecord(e0));
         LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
         const char *form = argc > 2 ? argv[2] : "whole";
@@ -53,8 +60,19 @@ int main(int argc, char **argv) {
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-        unsigned long long c[128];
+        unsigned long long c[128] = {0};
+#ifdef TFHE_SPIN_STATS
+        {
+            unsigned long long sp[4];
+            CK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_spin_stats), sizeof sp));
+            printf("rep %d: %.3f ms; gate-wave slot-wait polls that slept: %.3f per wave-step (%llu waves)\n", rep, ms,
+                   sp[0] / (double)(sp[1] ? sp[1] : 1) / P.n, sp[1]);
+            continue;
+        }
+#endif
+#ifdef TFHE_PHASE_PROF
         CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
+#endif
         if (O.br_form == 3) {  // latency form: per wave, per phase (ticks per step per gate)
             const char *wn[16] = {"fwd(other)", "barrier1", "sum", "barrier2", "inverse(other)", "barrier3", "tail", "-",
                                   "row: gather", "row: digits+twist", "row: fft", "row: terms", "inv: fft", "inv: untwist+add", "row: prefetch issue", "-"};

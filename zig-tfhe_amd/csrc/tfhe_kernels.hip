@@ -47,6 +47,9 @@ namespace tfhe {
 // defines TFHE_PHASE_PROF): s_memtime deltas per phase, summed per wave and
 // added to g_phase_cycles at the end.  Compiles to nothing otherwise.
 struct PhaseProf {
+#ifdef TFHE_SPIN_STATS
+    uint32_t spins = 0;
+#endif
 #ifdef TFHE_PHASE_PROF
     uint64_t last;
     int cur;
@@ -866,8 +869,11 @@ DEV bool lds_layout_bad(const void *smem) { return ((uint32_t)(size_t)(const lds
 #define TFHE_LOADER_PRIO 0
 #endif
 // `cap` >= 1 polls; on a timeout the loop falls through to `s_mov fail, 1`.
+#ifdef TFHE_SPIN_STATS  // development: polls that found the counter short, per wave (tools/phase_prof.hip)
+__device__ unsigned long long g_spin_stats[4];
+#endif
 template <int SLEEP = 1>
-DEV void spin_until_ge(const uint32_t *p, uint32_t target, uint32_t cap, uint32_t &fail) {
+DEV void spin_until_ge(const uint32_t *p, uint32_t target, uint32_t cap, uint32_t &fail, uint32_t *extra = nullptr) {
     // the poll loop in asm: every lane reads the same word, the loop stays
     // scalar, and hipcc sees one instruction (a compiler-visible loop here made
     // it hoist address arithmetic out of the step loop and spill)
@@ -890,6 +896,7 @@ DEV void spin_until_ge(const uint32_t *p, uint32_t target, uint32_t cap, uint32_
         : [v] "=&v"(v), [sv] "=&s"(sv), [cnt] "=&s"(cnt), [fail] "+s"(fail)
         : [addr] "v"(addr), [tgt] "s"(target), [cap] "s"(cap), [sl] "i"(SLEEP)
         : "memory", "scc");
+    if (extra) *extra += cap - cnt;  // spins that slept (cnt counts down per failed poll)
 }
 // One lane of a wave whose wait gave up ORs `bit` into the device error word
 // (a vector global atomic).  Called once per wave, after its loop.
@@ -1069,7 +1076,11 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
         if (FLAGS) {  // pair k = k0 + rp is use (k >> 1) of slot k & 1: wait until all 4 loaders published it
             const uint32_t k = k0 + (uint32_t)rp;
 #ifndef TFHE_KO_WAIT  // knock-out timing build: no wait for the pair's publication (wrong words possible)
+#ifdef TFHE_SPIN_STATS
+            spin_until_ge(sync + (k & 1), 4u * ((k >> 1) + 1u), spin_cap, fail, &pp.spins);
+#else
             spin_until_ge(sync + (k & 1), 4u * ((k >> 1) + 1u), spin_cap, fail);
+#endif
 #endif
             __builtin_amdgcn_sched_barrier(0);  // as the barrier did: nothing moves across the wait
         } else {
@@ -1315,6 +1326,12 @@ __global__ __launch_bounds__(LOADER ? 512 : 256, 1) void k_blind_rotate(
         for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], (unsigned long long)pp.acc[k]);
 #endif
     if (FLAGS) report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
+#ifdef TFHE_SPIN_STATS
+    if (t == 0) {
+        atomicAdd(&g_spin_stats[0], (unsigned long long)pp.spins);
+        atomicAdd(&g_spin_stats[1], 1ull);
+    }
+#endif
     if (FU) near_tie_flag(P, near, g, valid);
     // recompute: every wave of the workgroup read the flags before the prologue
     // barrier, so this item's flag can be cleared now; err[1] counts the items
