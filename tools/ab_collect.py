@@ -12,7 +12,8 @@ def main():
     head = sys.argv[3:]
     rows = []
     for f in sorted(glob.glob(f"gpurun_out/{tag}_*.json")):
-        m = re.match(rf"gpurun_out/{re.escape(tag)}_(.+?)(\d+)\.json$", f)
+        # variant names may end in digits (w0, md2): the round is the LAST digit run, rounds < 10
+        m = re.match(rf"gpurun_out/{re.escape(tag)}_(.+)(\d)\.json$", f)
         try:
             d = json.loads(open(f).read().splitlines()[-1])
         except (ValueError, IndexError):
