@@ -93,6 +93,8 @@ class Oracle:
         L.oracle_capture_rounded.argtypes = [C.c_void_p, C.c_size_t]
         L.oracle_set_fused.argtypes = [C.c_int]
         L.oracle_set_regroup.argtypes = [C.c_int]
+        L.oracle_set_fold.argtypes = [C.c_int]
+        L.oracle_folded_twiddles.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p]
         L.oracle_get_fused.restype = C.c_int
 
     # ---- cos/sin source of the twiddles (0 glibc, 1 fdlibm/musl; tfhe_oracle.c)
@@ -114,6 +116,17 @@ class Oracle:
         two fma chains from 0.0 added once (the pair and duo kernel forms); 2 = each
         row's product from 0.0, the six added in row order (the latency forms)."""
         self.lib.oracle_set_regroup(int(mode))
+
+    def set_fold(self, fold):
+        """Fused mode only: forward transforms with the twist folded into the stage
+        twiddles (evidence only: no kernel uses it)."""
+        self.lib.oracle_set_fold(int(bool(fold)))
+
+    def folded_twiddles(self, N=1024):
+        """The folded stage twiddles exp(i*pi*(1/2 - 2j)/len) at len/2 - 1 + j."""
+        re, im = np.zeros(N // 2 - 1), np.zeros(N // 2 - 1)
+        self.lib.oracle_folded_twiddles(N, re.ctypes.data, im.ctypes.data)
+        return re + 1j * im
 
     def rounded_values(self, fn, cap=1 << 16):
         """Run fn() and return the pre-rounding values its inverse transforms

@@ -253,6 +253,28 @@ static int g_fused = 0, g_guard = 0;
  * own fma chain from 0.0, and the six products are added in row order. */
 static int g_regroup = 0;
 void oracle_set_regroup(int mode) { g_regroup = mode == 2 ? 2 : mode ? 1 : 0; }
+/* Folded twist (evidence only; no kernel uses it):
+ * fused mode only.  The forward transform takes the digit pairs
+ * untwisted and every stage-len butterfly j multiplies by the folded twiddle
+ * exp(i*pi*(1/2 - 2j)/len) = W_len^j * twist[512/len] instead of the
+ * recurrence W_len^j: the twist of each sub-transform's second half, relative
+ * to its first half's, rides on the butterfly, and the whole transform's root
+ * (index 0) carries twist 1.  Exact in real arithmetic, 108 f64 instructions
+ * fewer per CMUX, but its rounding errors are independent of the reference's:
+ * on adversarial digits the values part by more than the margin guard's 1/4
+ * (tests/test_oracle.py::test_folded_twist_decorrelates_from_the_reference). */
+static int g_fold = 0;
+void oracle_set_fold(int fold) { g_fold = fold ? 1 : 0; }
+/* the folded twiddle of stage len, j */
+void oracle_folded_twiddles(uint32_t N, double *re, double *im) {
+    size_t n = N / 2;
+    for (size_t len = 2; len <= n; len *= 2)
+        for (size_t j = 0; j < len / 2; j++) {
+            double a = (0.5 - 2.0 * (double)j) * (PI_F64 / (double)len);
+            re[len / 2 - 1 + j] = tw_cos(a);
+            im[len / 2 - 1 + j] = tw_sin(a);
+        }
+}
 static __thread int tl_force_ref = 0, tl_near = 0;
 #define FUSED (g_fused && !tl_force_ref)
 void oracle_set_fused(int fused) {
@@ -312,8 +334,9 @@ static void bit_reverse_radix2(cplx *data, size_t n) {
     }
 }
 
-/* radix2FFT — fft.zig:582-619 (reached through fftInPlace, :515-521) */
-static void radix2_fft(cplx *data, size_t n, int inverse) {
+/* radix2FFT — fft.zig:582-619 (reached through fftInPlace, :515-521).
+ * fold (fused forward only): the folded twiddles instead of the recurrence. */
+static void radix2_fft_ex(cplx *data, size_t n, int inverse, const double *fre, const double *fim) {
     bit_reverse_radix2(data, n);
     for (size_t len = 2; len <= n; len *= 2) {
         double angle = inverse ? 2.0 * PI_F64 / (double)len : -2.0 * PI_F64 / (double)len;
@@ -322,6 +345,10 @@ static void radix2_fft(cplx *data, size_t n, int inverse) {
         for (size_t i = 0; i < n; i += len) {
             double w_re = 1.0, w_im = 0.0;
             for (size_t j = 0; j < len / 2; j++) {
+                if (fre) {
+                    w_re = fre[len / 2 - 1 + j];
+                    w_im = fim[len / 2 - 1 + j];
+                }
                 cplx u = data[i + j];
                 cplx x = data[i + j + len / 2];
                 if (FUSED) {                               /* a = u + x*w, b = 2u - a */
@@ -347,6 +374,7 @@ static void radix2_fft(cplx *data, size_t n, int inverse) {
         }
     }
 }
+static void radix2_fft(cplx *data, size_t n, int inverse) { radix2_fft_ex(data, n, inverse, NULL, NULL); }
 
 /* The per-stage recurrence values w_j used by radix2FFT (same for every block
  * i of a stage), exported so tests can pin the GPU twiddle tables to them.
@@ -374,6 +402,21 @@ void oracle_ifft(uint32_t N, const uint32_t *in, double *out) {
     cplx *buf = (cplx *)malloc(sizeof(cplx) * n2);
     double *tre = (double *)malloc(sizeof(double) * n2), *tim = (double *)malloc(sizeof(double) * n2);
     get_twist(N, tre, tim);
+    if (FUSED && g_fold) {  /* untwisted input, folded stage twiddles */
+        double *fre = (double *)malloc(sizeof(double) * n2), *fim = (double *)malloc(sizeof(double) * n2);
+        oracle_folded_twiddles(N, fre, fim);
+        for (size_t i = 0; i < n2; i++) {
+            buf[i].re = (double)(int32_t)in[i];
+            buf[i].im = (double)(int32_t)in[i + n2];
+        }
+        radix2_fft_ex(buf, n2, 0, fre, fim);
+        for (size_t i = 0; i < n2; i++) {
+            out[i] = buf[i].re * 2.0;
+            out[i + n2] = buf[i].im * 2.0;
+        }
+        free(fre); free(fim); free(buf); free(tre); free(tim);
+        return;
+    }
     for (size_t i = 0; i < n2; i++) {
         double in_re = (double)(int32_t)in[i];
         double in_im = (double)(int32_t)in[i + n2];

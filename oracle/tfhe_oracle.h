@@ -147,6 +147,8 @@ double oracle_trig_sin(double x, int source);
 void oracle_set_fused(int fused);
 void oracle_set_regroup(int mode);  /* fused mode: 1 = (rows of a) + (rows of b) (pair/duo forms), 2 = per-row terms summed (latency forms) */
 int oracle_get_fused(void);
+void oracle_set_fold(int fold);  /* fused mode: forward transforms with the folded twist (evidence only) */
+void oracle_folded_twiddles(uint32_t N, double *re, double *im);
 /* max |x - round(x)| rounded by oracle_fft on this thread since the last call (then reset) */
 double oracle_take_round_error(void);
 /* Start capturing the inverse transforms' pre-rounding values into buf (pairs

@@ -233,18 +233,21 @@ def _tmp_with_fields(oracle, p, fields):
 def _ext_values(oracle, p, rows, x, mode):
     """Pre-rounding values and words of externalProductWithFft with integer rows
     (2L, 2, N) in `mode` (0 reference trees, 1 fused, 3 fused with the pair / duo
-    forms' regrouped row sums, 4 fused with the latency forms' summed row terms)."""
+    forms' regrouped row sums, 4 fused with the latency forms' summed row terms,
+    5 fused with folded-twist forward transforms, which no kernel uses)."""
     off = oracle.decomposition_offset(p)
     trgsw = np.array([[oracle.ifft((r[0] % (1 << 32)).astype(np.uint32)),
                        oracle.ifft((r[1] % (1 << 32)).astype(np.uint32))] for r in rows])
     try:
-        oracle.set_fused(1 if mode in (3, 4) else mode)
+        oracle.set_fused(1 if mode in (3, 4, 5) else mode)
         oracle.set_regroup({3: 1, 4: 2}.get(mode, 0))
+        oracle.set_fold(mode == 5)
         out = {}
         v = oracle.rounded_values(lambda: out.setdefault("w", oracle.external_product(p, trgsw, x, off)))
     finally:
         oracle.set_fused(0)
         oracle.set_regroup(False)
+        oracle.set_fold(False)
     return v, out["w"]
 
 
@@ -354,6 +357,48 @@ def test_aligned_adversarial_digits_part_the_trees(oracle):
     assert delta < 0.125  # half the guard's 1/4 margin
     assert part > 0
     assert delta_rg < 0.125
+
+
+def test_folded_twist_decorrelates_from_the_reference(oracle):
+    """Why the fused kernels keep the reference's twist and recurrence twiddles
+    (DESIGN.md §6.1, round 4).  Folding the twist into the stage twiddles (forward
+    butterfly j of stage len by exp(i*pi*(1/2 - 2j)/len), untwisted input: 108 f64
+    instructions fewer per CMUX) is exact in real arithmetic and rounds honest
+    rotations to the same words, but on the aligned adversarial digits its
+    pre-rounding values part from the reference's by more than the guard's 1/4
+    (the fused trees, same twiddles and order, stay within 1/16: their rounding
+    errors are the reference's, not independent ones), so the margin guard would
+    no longer cover it.  Oracle mode 5 restates it; no kernel uses it."""
+    from oracle import params
+    p = params("128")
+    off = oracle.decomposition_offset(p)
+    g = rng(607)
+
+    def tmp3(f0, f1, f2):
+        v = (f0.astype(np.uint64) << 26) | (f1.astype(np.uint64) << 20) | (f2.astype(np.uint64) << 14)
+        return ((v - off) % (1 << 32)).astype(np.uint32)
+
+    d_fused = d_fold = 0.0
+    for trial in range(40):
+        rows = g.integers(-(1 << 31), 1 << 31, (2 * p.L, 2, 1024))
+        k = int(g.integers(0, 1024))
+        j = np.arange(1024)
+        m, w = (k - j) % 1024, np.where(j <= k, 1, -1)
+        F = [np.where(w * np.sign(rows[i][trial % 2][m]) > 0, 63, 0) for i in range(2 * p.L)]
+        x = np.concatenate([tmp3(F[0], F[1], F[2]), tmp3(F[3], F[4], F[5])])
+        v0, _ = _ext_values(oracle, p, rows, x, 0)
+        v1, _ = _ext_values(oracle, p, rows, x, 1)
+        v5, _ = _ext_values(oracle, p, rows, x, 5)
+        d_fused = max(d_fused, float(np.abs(v0 - v1).max()))
+        d_fold = max(d_fold, float(np.abs(v0 - v5).max()))
+    assert d_fused <= 0.0625 + 1e-12
+    assert d_fold > 0.25
+    # the folded twiddles are the exact products W_len^j * twist[512/len] (to 1 ulp)
+    tw = oracle.folded_twiddles(1024)
+    for ln in (2, 8, 512):
+        for jj in (0, ln // 4, ln // 2 - 1):
+            want = np.exp(-2j * np.pi * jj / ln) * np.exp(1j * np.pi * (512 // ln) / 1024)
+            assert abs(tw[ln // 2 - 1 + jj] - want) < 4e-16
 
 
 FUSED_BK_SPECTRUM_MAX = 2.0 ** 39  # tfhe_gpu.cpp key_admission (DESIGN.md §6.1)
