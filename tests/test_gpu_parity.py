@@ -730,3 +730,35 @@ def test_margin_guard_quiet_on_honest_batches(oracle):
     out = c.gate_batch(np.zeros(1024, np.uint8), A, B)
     assert c.near_tie_items() == before
     assert np.array_equal(sk.decrypt_bool(out), ~(a.astype(bool) & b.astype(bool)))
+
+
+@pytest.mark.parametrize("pname", ["128", "80"])
+def test_fused_equals_reference_soak_all_gates(oracle, pname):
+    """Soak of the default arithmetic at scale: 65,536 gate bootstraps of every
+    op (the ten gates in turn) over fresh encryptions, in 16 batches of 4,096
+    (whole form, every CU), fused (the default) against the reference's
+    expression trees on the same device: identical words for every gate, the
+    truth tables decrypt, and the margin guard's recompute counter moves by at
+    most a handful (honest rotations stay ~0.1 from an integer). Complements
+    the oracle comparisons, which the CPU's speed caps at small batches."""
+    c, k = ctx_for(oracle, pname)
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    g = rng(7070 + int(pname))
+    B = 4096
+    before = c.near_tie_items()
+    for rep in range(16):
+        a, b = g.integers(0, 2, B).astype(np.uint8), g.integers(0, 2, B).astype(np.uint8)
+        ops = ((np.arange(B) + rep) % 10).astype(np.uint8)
+        A, Bc = sk.encrypt_bool(a, seed0=700_000 + 2 * rep), sk.encrypt_bool(b, seed0=700_001 + 2 * rep)
+        fused = c.gate_batch(ops, A, Bc)
+        assert "fused" in c.last_kernels()
+        with c.options(arith=tfhe_amd.ARITH_REFERENCE):
+            ref = c.gate_batch(ops, A, Bc)
+        assert np.array_equal(fused, ref), f"rep {rep}: {(fused != ref).any(axis=1).sum()} gates differ"
+        if rep == 0:
+            want = np.zeros(B, bool)
+            for o in range(10):
+                m = ops == o
+                want[m] = TRUTH[o](a.astype(bool)[m], b.astype(bool)[m])
+            assert np.array_equal(sk.decrypt_bool(fused), want)
+    assert c.near_tie_items() - before <= 4
