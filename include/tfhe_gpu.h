@@ -143,7 +143,8 @@ int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
  * fastest forms).  Set on a context before use; a multi-device context
  * passes them to every device.  TFHE_ERR_INVALID for an unknown key or value. */
 enum {
-    TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 2 split, 3 latency, 4 pair,
+    TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 3 latency (2 split and
+                                     4 pair were removed in round 4: TFHE_ERR_INVALID),
                                      5 octo (8 items per workgroup, two gate waves per SIMD), 6 duo (two
                                      computing waves per item on one SIMD, no barriers in the step loop),
                                      7 the latency form with split transforms at L = 3 (measured slower,

@@ -113,7 +113,7 @@ def test_key_switch_gemm_full_batches(oracle, B):
 
 # ---- blind rotation / bootstrap ---------------------------------------------
 @pytest.mark.parametrize("form", ["whole", "whole-noloader", "whole-reference", "whole-noloader-reference",
-                                  "whole-barrier", "whole-barrier-reference", "split", "wide", "pair", "pair-reference",
+                                  "whole-barrier", "whole-barrier-reference", "wide",
                                   "octo", "octo-reference", "duo", "duo-reference", "wide-reference", "wide2",
                                   "wide2-reference"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
@@ -131,11 +131,9 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
         assert np.array_equal(c.blind_rotate_batch(cts), want)
         if form.startswith("whole"):  # fused arithmetic only where the external product is exact (SMALL)
             assert c.last_kernels().endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
-        if form.startswith("pair"):  # L = 1 (UINT4) runs the pair form in the reference's trees too
-            assert c.last_kernels().startswith("k_blind_rotate_pair<") == (pname == "uint4" or form == "pair")
-        if form.startswith("duo"):  # the same rule for the duo form
+        if form.startswith("duo"):  # L = 1 (UINT4) runs the duo form in the reference's trees too
             assert c.last_kernels().startswith("k_blind_rotate_duo<") == (pname == "uint4" or form == "duo")
-        prefix = {"whole": "k_blind_rotate<", "split": "k_blind_rotate_split<", "octo": "k_blind_rotate_octo<",
+        prefix = {"whole": "k_blind_rotate<", "octo": "k_blind_rotate_octo<",
                   # wide2 (split transforms) exists at L = 3; UINT4 (L = 1) runs the round-3 latency form
                   "wide": "k_blind_rotate_wide<",
                   "wide2": "k_blind_rotate_wide2<" if pname != "uint4" else "k_blind_rotate_wide<"}
@@ -144,7 +142,7 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
-@pytest.mark.parametrize("form,loader,sync", [("whole", 1, 1), ("whole", 1, 0), ("whole", 0, 0), ("pair", 1, 0),
+@pytest.mark.parametrize("form,loader,sync", [("whole", 1, 1), ("whole", 1, 0), ("whole", 0, 0),
                                               ("octo", 1, 0), ("duo", 1, 0)])
 def test_whole_form_every_idle_slot_count(oracle, form, loader, sync):
     """Whole form at B = 1..8: the last workgroup has 3, 2, 1 or 0 idle gate slots
@@ -160,7 +158,7 @@ def test_whole_form_every_idle_slot_count(oracle, form, loader, sync):
             assert np.array_equal(c.blind_rotate_batch(cts[:B]), want[:B]), B
 
 
-@pytest.mark.parametrize("form", ["whole", "split", "wide"])
+@pytest.mark.parametrize("form", ["whole", "octo", "wide"])
 def test_bootstrap_without_key_switch(oracle, form):
     """VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69) and the
     strategy mirror: blind rotation + the hybrid sampleExtractIndex2."""
@@ -603,6 +601,8 @@ def test_options_validation_and_report(oracle):
     with pytest.raises(tfhe_amd.TfheError):
         c.set_option("br_form", 9)
     assert c.lib.tfhe_gpu_set_option(c.h, 99, 0) == -1
+    for removed in (2, 4):  # the split and pair forms, removed in round 4
+        assert c.lib.tfhe_gpu_set_option(c.h, 1, removed) == -1
     assert c.get_option("br_form") == 0
     g = rng(91)
     cts = u32rand(g, 3, k.p.n + 1)
@@ -642,7 +642,7 @@ def test_slot_counters_and_barrier_agree_at_full_size(oracle):
         assert np.array_equal(sk.decrypt_bool(flags), ~(a_bits.astype(bool) & b_bits.astype(bool)))
 
 
-@pytest.mark.parametrize("form", ["auto", "whole", "split", "pair", "wide", "octo", "duo"])
+@pytest.mark.parametrize("form", ["auto", "whole", "wide", "octo", "duo"])
 def test_margin_guard_recomputes_near_ties(oracle, form):
     """under a crafted key (conftest.crafted_near_tie_case) the
     unguarded fused arithmetic parts from the reference (the oracle's fused mode

@@ -12,7 +12,7 @@ for B in [1, 8, 64, 128, 256, 512, 1024]:
     Bc = sk.encrypt_bool(g.integers(0, 2, B).astype(np.uint8), seed0=9999)
     ops = np.zeros(B, np.uint8)
     row = [f"B={B:5d}"]
-    for form in ["whole", "split", "wide"]:
+    for form in ["whole", "octo", "wide"]:
         c.set_option("br_form", form)
         c.gate_batch(ops, A, Bc)
         t0 = time.perf_counter()

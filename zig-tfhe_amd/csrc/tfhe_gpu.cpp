@@ -1679,7 +1679,7 @@ namespace {
 bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     bool ok = false;
     switch (key) {
-    case TFHE_OPT_BR_FORM: ok = v >= 0 && v <= 7; break;
+    case TFHE_OPT_BR_FORM: ok = v >= 0 && v <= 7 && v != 2 && v != 4; break;  // 2 split, 4 pair: removed in round 4
     case TFHE_OPT_KS_FORM: ok = v >= 0 && v <= 3; break;
     case TFHE_OPT_BR_LOADER:
     case TFHE_OPT_KS_NARROW:

@@ -1602,37 +1602,11 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_octo(
     }
 }
 
-// ---------------------------------------------------------------------------
-// Blind rotation, split form: TWO wavefronts per item, 4 items per 512-thread
-// block (2 waves per SIMD).  Wave h of an item owns accumulator polynomial h
-// (h = 0: a, 1: b) for the tmp / inverse / update phases.  The 2L decomposed
-// rows are dealt out interleaved: in round r wave h forward-transforms row
-// 2r + h (polynomial (2r+h)/L, level (2r+h)%L; it reads the partner's tmp from
-// LDS when the row belongs to the other polynomial) and publishes the spectrum.
-// Round r thus holds rows 2r and 2r+1 — consecutive — so every wave adds both
-// terms to its output polynomial in the reference's row order 0..2L-1 with no
-// terms held across rounds.  Finally each wave inverse-transforms its own
-// output and updates its own polynomial.
-// ---------------------------------------------------------------------------
-constexpr int BS_GATES = 4;
-constexpr int BS_WAVES = 2 * BS_GATES;
-constexpr int BS_LDS_BK = 2 * 1024 * 16;   // rows 2r and 2r+1, double2
-constexpr int BS_LDS_TW = 512 * 16;
-constexpr int BS_LDS_TWIST = 512 * 16;
-constexpr int BS_LDS_ACC = 1024 * 4;       // per wave: its polynomial (then its digits' source)
-constexpr int BS_LDS_X = 512 * 16;         // per wave: FFT exchanges, then its spectrum
-constexpr int BS_LDS_AT = 1024 * 2;        // per item
-constexpr int BS_LDS_TOTAL =
-    BS_LDS_BK + BS_LDS_TW + BS_LDS_TWIST + BS_WAVES * (BS_LDS_ACC + BS_LDS_X) + BS_GATES * BS_LDS_AT + 64;
-
-// LDS-DMA of rows (2r, 2r+1) of BK[i] (contiguous 32 KB): 512 threads x 4.
-DEV void issue_bk_rows(const double2 *__restrict__ rows, double2 *lds, int tid) {
-    const int wbase = tid & ~63;
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-        __builtin_amdgcn_global_load_lds((global_void_t *)(rows + 512 * c + tid),
-                                         (lds_void_t *)(lds + 512 * c + wbase), 16, 0, 0);
-}
+// The split form (two waves per item, each transforming every other row) and
+// the pair form (two waves per item, one per accumulator polynomial, with the
+// regrouped row sums the duo form kept) were removed in round 4: measured
+// slower than the whole form at every batch and parameter set since rounds 1
+// and 2 (DESIGN.md §4.3, §4.3b record their measurements).
 
 // term = D * BK row part (fmaInFd1024's (a_re*b_re - a_im*b_im, a_re*b_im + a_im*b_re));
 // FU: one multiply and one fma per component
@@ -1640,381 +1614,6 @@ template <bool FU = false>
 DEV C2 cmul_bk(C2 d, double2 k) {
     if (FU) return c2(fmad(d.x, k.x, -(d.y * k.y)), fmad(d.x, k.y, d.y * k.x));
     return c2(d.x * k.x - d.y * k.y, d.x * k.y + d.y * k.x);
-}
-
-template <int L, bool SMALL, bool FU = false>
-__global__ __launch_bounds__(512, 2) void k_blind_rotate_split(
-    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
-    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
-    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[BS_LDS_TOTAL];
-    const int tid = threadIdx.x;
-    const int t = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int gs = w >> 1;  // item slot in the block
-    const int h = w & 1;    // polynomial owned by this wave
-    double2 *s_bk = reinterpret_cast<double2 *>(smem);
-    C2 *s_tw = reinterpret_cast<C2 *>(smem + BS_LDS_BK);
-    C2 *s_twist = reinterpret_cast<C2 *>(smem + BS_LDS_BK + BS_LDS_TW);
-    unsigned char *base = smem + BS_LDS_BK + BS_LDS_TW + BS_LDS_TWIST;
-    uint32_t *s_acc = reinterpret_cast<uint32_t *>(base + w * BS_LDS_ACC);
-    C2 *s_xg = reinterpret_cast<C2 *>(base + BS_WAVES * BS_LDS_ACC + (2 * gs) * BS_LDS_X);  // item's pair
-    C2 *s_x = s_xg + h * 512;
-    uint16_t *s_at = reinterpret_cast<uint16_t *>(base + BS_WAVES * (BS_LDS_ACC + BS_LDS_X) + gs * BS_LDS_AT);
-    int *s_bt = reinterpret_cast<int *>(base + BS_WAVES * (BS_LDS_ACC + BS_LDS_X) + BS_GATES * BS_LDS_AT);
-
-    const int n = P.n;
-    const size_t g_raw = (size_t)blockIdx.x * BS_GATES + gs;
-    const bool valid = g_raw < B;
-    const size_t g = valid ? g_raw : B - 1;
-    // idx (optional): item g reads ciphertexts idx[2g] of in_a and idx[2g+1] of in_b
-    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
-    const uint32_t *A = in_a + ia * (size_t)(n + 1);
-    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
-    const int op = ops ? (int)ops[g] : 255;
-    const size_t trgsw = (size_t)2 * L * 1024;  // double2 per BK[i]
-
-    issue_bk_rows(bkd, s_bk, tid);  // step 0, round 0
-    for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
-    for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
-    if (h == 0) {
-        for (int i = t; i <= n; i += 64) {
-            uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
-            uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
-            if (i < n) s_at[i] = (uint16_t)tl;
-            else s_bt[gs] = 2048 - (int)tl;
-        }
-    }
-    __syncthreads();
-    const int bt = __builtin_amdgcn_readfirstlane(s_bt[gs]);
-    const uint32_t *tv = testvec + h * 1024;
-    uint32_t acc[16];  // own polynomial at coefficients t + 64m
-#pragma unroll
-    for (int m = 0; m < 16; m++) {
-        acc[m] = rot_read(tv, t + 64 * m, bt);
-        s_acc[t + 64 * m] = acc[m];
-    }
-    LdsTw T;
-    T.init(s_tw, TT);
-    const C2 *twist_t = s_twist + t;
-    const C2 *spec_0 = s_xg;        // spectrum of row 2r (wave 0 of the item)
-    const C2 *spec_1 = s_xg + 512;  // spectrum of row 2r+1 (wave 1)
-    const uint32_t *s_tmp_item = reinterpret_cast<const uint32_t *>(base + (2 * gs) * BS_LDS_ACC);
-    uint32_t near = NEAR_NONE;  // FU: margin guard
-    wave_sync();
-
-    for (int i = 0; i < n; i++) {
-        const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
-        // own tmp = X^{a~} p - p + offset, staged over the polynomial's LDS copy
-        uint32_t tm[16];
-#pragma unroll
-        for (int m = 0; m < 16; m++) tm[m] = rot_read(s_acc, t + 64 * m, at) - acc[m] + P.offset;
-        wave_sync();
-#pragma unroll
-        for (int m = 0; m < 16; m++) s_acc[t + 64 * m] = tm[m];
-        __syncthreads();  // both tmps visible to both waves of the item
-        C2 S[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) S[q] = c2(0.0, 0.0);  // the reference's zeroed accumulator
-#pragma unroll 1
-        for (int r = 0; r < L; r++) {
-            const int row = 2 * r + h;
-            const int poly = row >= L ? 1 : 0;
-            const int level = row - poly * L;
-            C2 d[1][8];
-            const uint32_t *src = s_tmp_item + poly * 1024 + t;
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int m = br3(q);
-                d[0][q] = twist_in<FU>(digit_f64(src[64 * m], level, P.bgbit),
-                                   digit_f64(src[64 * (m + 8)], level, P.bgbit), twist_t[64 * m]);
-            }
-#ifndef TFHE_KO_FFT
-            fft512<1, false, FU>(d, s_x, T, t);
-#endif
-#pragma unroll
-            for (int q = 0; q < 8; q++) s_x[t + 64 * q] = d[0][q];  // publish this row's spectrum
-#ifndef TFHE_KO_BAR
-            __syncthreads();  // spectra of rows 2r, 2r+1 and BK rows 2r, 2r+1 are in LDS
-#endif
-#ifndef TFHE_KO_MAC
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const C2 t0 = cmul_bk<FU>(spec_0[t + 64 * q], s_bk[(2 * q + h) * 64 + t]);
-                const C2 t1 = cmul_bk<FU>(spec_1[t + 64 * q], s_bk[1024 + (2 * q + h) * 64 + t]);
-                S[q] = c2(S[q].x + t0.x, S[q].y + t0.y);
-                S[q] = c2(S[q].x + t1.x, S[q].y + t1.y);
-            }
-#else
-            for (int q = 0; q < 8; q++) S[q] = c2(S[q].x + d[0][q].x, S[q].y);
-#endif
-#ifndef TFHE_KO_BAR
-            __syncthreads();  // spectra and BK rows consumed
-#endif
-            if (r + 1 < L) issue_bk_rows(bkd + (size_t)i * trgsw + (size_t)(2 * r + 2) * 1024, s_bk, tid);
-            else if (i + 1 < n) issue_bk_rows(bkd + (size_t)(i + 1) * trgsw, s_bk, tid);
-        }
-        // inverse transform of the own output polynomial, acc' = ExtProd + acc
-        C2 e[1][8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) e[0][q] = S[br3(q)];
-#ifndef TFHE_KO_INV
-        fft512<1, true, FU>(e, s_x, T, t);
-#endif
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            double re, im;
-            untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-            acc[q] += to_torus<SMALL, FU>(re, near);
-            acc[q + 8] += to_torus<SMALL, FU>(im, near);
-        }
-        wave_sync();
-#pragma unroll
-        for (int m = 0; m < 16; m++) s_acc[t + 64 * m] = acc[m];
-        wave_sync();
-    }
-    if (FU) near_tie_flag(P, near, g, valid);
-
-    if (!valid) return;
-    if (out_mode == BR_OUT_LV1) {
-        // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
-        uint32_t *o = out + g * (size_t)1025;
-        if (h == 0) {
-            for (int j = t; j < 1024; j += 64) o[j] = j == 0 ? s_acc[0] : 0u - s_acc[1024 - j];
-        } else if (t == 0) {
-            o[1024] = s_acc[0];
-        }
-    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {
-        // sampleExtractIndex2(acc, 0) over the lv0 length n (trlwe.zig:165-180)
-        uint32_t *o = out + g * (size_t)(n + 1);
-        if (h == 0) {
-            for (int j = t; j < n; j += 64) o[j] = j == 0 ? s_acc[0] : 0u - s_acc[n - j];
-        } else if (t == 0) {
-            o[n] = s_acc[0];
-        }
-    } else {
-        uint32_t *o = out + g * (size_t)2048 + h * 1024;
-        for (int j = t; j < 1024; j += 64) o[j] = s_acc[j];
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Blind rotation, "pair" form: TWO waves per item, 4 items per 512-thread
-// workgroup, so every SIMD runs two waves that both do f64 work (the whole
-// form runs one gate wave per SIMD; its second wave only issues DMAs).  Wave
-// (g, h) of item g owns accumulator polynomial h (0: a, 1: b) and its L
-// decomposition rows (rows hL .. hL+L-1): per CMUX step it
-//   1. gathers X^a~ * acc_h - acc_h (+ offset) from its own LDS buffer (the
-//      rotation touches only its own polynomial: no cross-wave dependence);
-//   2. for each level r: digits in registers, forward FFT, and the MAC of that
-//      row against both BK output halves (a, b) into partial sums P_h,a / P_h,b;
-//      the BK slot holds rows r and L+r, one LDS-DMA of 32 KB per level, double
-//      buffered, published by the level's block barrier;
-//   3. hands the partial its partner needs (h = 0 gives P_0,b, h = 1 gives
-//      P_1,a): it writes it into the PARTNER's buffer, idle since the last
-//      level's barrier (every wave's last forward FFT is done), and after one
-//      barrier reads the partner's contribution from its own buffer, which
-//      nobody else touches until the next step; adds it to its own partial,
-//      inverse-transforms output polynomial h and updates acc_h.
-// Output h's spectrum is (sum over rows 0..L-1) + (sum over rows L..2L-1):
-// for L = 1 that is the reference's row order exactly (0 + t0 = t0, then
-// t0 + t1), so the form is exact with the reference's expression trees too;
-// for L > 1 the grouping differs from the reference's running sum, which is
-// only allowed in the exact-integer regime (FU).
-// LDS: BK 2 x 32 KB + twiddles 8 KB + twist 8 KB + 8 wave buffers x 8 KB
-// (exchange / accumulator staging / hand-off) + 4 x 2 KB a~ = 152 KB.
-// ---------------------------------------------------------------------------
-constexpr int BP_GATES = 4;
-constexpr int BP_WAVES = 2 * BP_GATES;
-constexpr int BP_LDS_BK = 2 * 2048 * 16;   // two slots of (row r, row L+r), double2
-constexpr int BP_LDS_TW = 512 * 16;
-constexpr int BP_LDS_TWIST = 512 * 16;
-constexpr int BP_LDS_X = 512 * 16;         // per wave
-constexpr int BP_LDS_AT = 1024 * 2;        // per item
-constexpr int BP_LDS_TOTAL = BP_LDS_BK + BP_LDS_TW + BP_LDS_TWIST + BP_WAVES * BP_LDS_X + BP_GATES * BP_LDS_AT + 64;
-
-// LDS-DMA of rows (r, L+r) of one BK[i] (16 KB each, not adjacent in the device
-// layout) into a 32 KB slot: 512 threads x 4 pieces of 16 B; hand-counted
-// completion like issue_bk_pair_async.
-DEV void issue_bk_split_async(const double2 *__restrict__ row_lo, const double2 *__restrict__ row_hi, double2 *slot,
-                              int tid) {
-    const uint32_t base = (uint32_t)(size_t)(lds_void_t *)slot + (uint32_t)(tid & ~63) * 16;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const double2 *src = (k < 2 ? row_lo : row_hi) + 512 * (k & 1) + tid;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(base + 512 * 16 * k);
-        uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(src), "s"(dst)
-            : "memory");
-    }
-}
-
-template <int L, bool SMALL, bool FU>
-__global__ __launch_bounds__(512, 1) void k_blind_rotate_pair(
-    KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
-    const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
-    const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
-    static_assert(FU || L == 1, "regrouped row sums need the exact-integer regime");
-    __shared__ __attribute__((aligned(16))) unsigned char smem[BP_LDS_TOTAL];
-    const int tid = threadIdx.x;
-    const int t = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int gs = w & 3;   // item slot
-    const int h = w >> 2;   // output polynomial / row half owned by this wave
-    double2 *s_bk = reinterpret_cast<double2 *>(smem);
-    C2 *s_tw = reinterpret_cast<C2 *>(smem + BP_LDS_BK);
-    C2 *s_twist = reinterpret_cast<C2 *>(smem + BP_LDS_BK + BP_LDS_TW);
-    unsigned char *xbase = smem + BP_LDS_BK + BP_LDS_TW + BP_LDS_TWIST;
-    C2 *s_x = reinterpret_cast<C2 *>(xbase + w * BP_LDS_X);
-    C2 *s_xp = reinterpret_cast<C2 *>(xbase + (w ^ 4) * BP_LDS_X);  // partner's buffer
-    uint32_t *s_xw = reinterpret_cast<uint32_t *>(s_x);
-    uint16_t *s_at = reinterpret_cast<uint16_t *>(xbase + BP_WAVES * BP_LDS_X + gs * BP_LDS_AT);
-    int *s_bt = reinterpret_cast<int *>(xbase + BP_WAVES * BP_LDS_X + BP_GATES * BP_LDS_AT);
-
-    const int n = P.n;
-    const size_t g_raw = (size_t)blockIdx.x * BP_GATES + gs;
-    const bool valid = g_raw < B;
-    const size_t g = valid ? g_raw : B - 1;  // ragged tail: compute a copy, store nothing
-    const size_t ia = idx ? idx[2 * g] : g, ib = idx ? idx[2 * g + 1] : g;
-    const uint32_t *A = in_a + ia * (size_t)(n + 1);
-    const uint32_t *Bv = in_b ? in_b + ib * (size_t)(n + 1) : A;
-    const int op = ops ? (int)ops[g] : 255;
-    const size_t step = (size_t)2 * L * 1024;  // double2 per BK[i]
-
-    issue_bk_split_async(bkd, bkd + (size_t)L * 1024, s_bk, tid);  // step 0, level 0 into slot 0
-    for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
-    for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
-    if (h == 0) {  // a~_i, b~ (trgsw.zig:297, :312), 64-bit adds
-        for (int i = t; i <= n; i += 64) {
-            uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
-            uint32_t tl = (uint32_t)(((uint64_t)c + (1ull << 20)) >> 21);
-            if (i < n) s_at[i] = (uint16_t)tl;
-            else s_bt[gs] = 2048 - (int)tl;
-        }
-    }
-    __syncthreads();
-    const int bt = __builtin_amdgcn_readfirstlane(s_bt[gs]);
-    uint32_t acc[16];  // own polynomial h at coefficients t + 64m
-#pragma unroll
-    for (int m = 0; m < 16; m++) acc[m] = rot_read(testvec + h * 1024, t + 64 * m, bt);
-    LdsTw T;
-    T.init(s_tw, TT);
-    const C2 *twist_t = s_twist + t;
-    int at_next = s_at[0];
-    uint32_t near = NEAR_NONE;  // FU: margin guard
-
-    for (int i = 0; i < n; i++) {
-        const int at = __builtin_amdgcn_readfirstlane(at_next);
-        at_next = s_at[i + 1 < n ? i + 1 : i];
-        // tmp = X^{a~} acc_h - acc_h + offset, staged through this wave's buffer
-        uint32_t tmp[16];
-#pragma unroll
-        for (int m = 0; m < 16; m++) s_xw[t + 64 * m] = acc[m];
-        wave_sync();
-        const int rb = (t - at) & 2047;
-#pragma unroll
-        for (int m = 0; m < 16; m++) tmp[m] = s_xw[(rb + 64 * m) & 1023];
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int m = 0; m < 16; m++) {
-            const bool neg = ((rb + 64 * m) & 1024) != 0;
-            tmp[m] = (neg ? 0u - tmp[m] : tmp[m]) - acc[m] + P.offset;
-        }
-        wave_sync();  // the buffer becomes the FFT exchange buffer
-        C2 pa[8], pb[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            pa[q] = c2(0.0, 0.0);
-            pb[q] = c2(0.0, 0.0);
-        }
-#pragma unroll 1
-        for (int r = 0; r < L; r++) {
-            C2 d[1][8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int m = br3(q);
-                d[0][q] = twist_in<FU>(digit_f64(tmp[m], r, P.bgbit), digit_f64(tmp[m + 8], r, P.bgbit),
-                                       twist_t[64 * m]);
-            }
-            fft512<1, false, FU>(d, s_x, T, t);
-            const int slot = (L * i + r) & 1;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's pieces of the level landed
-            __syncthreads();  // level r's rows are in `slot`; everyone is done with the other slot
-            if (r + 1 < L)
-                issue_bk_split_async(bkd + (size_t)i * step + (size_t)(r + 1) * 1024,
-                                     bkd + (size_t)i * step + (size_t)(L + r + 1) * 1024, s_bk + (slot ^ 1) * 2048, tid);
-            else if (i + 1 < n)
-                issue_bk_split_async(bkd + (size_t)(i + 1) * step, bkd + (size_t)(i + 1) * step + (size_t)L * 1024,
-                                     s_bk + (slot ^ 1) * 2048, tid);
-            // row hL + r: [q][a|b][lane] at half h of the slot
-            const double2 *bk = s_bk + slot * 2048 + h * 1024;
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const double2 ka = bk[(2 * q) * 64 + t], kb = bk[(2 * q + 1) * 64 + t];
-                const C2 x = d[0][q];
-                if (FU) {
-                    pa[q] = c2(fmad(x.x, ka.x, fmad(-x.y, ka.y, pa[q].x)), fmad(x.x, ka.y, fmad(x.y, ka.x, pa[q].y)));
-                    pb[q] = c2(fmad(x.x, kb.x, fmad(-x.y, kb.y, pb[q].x)), fmad(x.x, kb.y, fmad(x.y, kb.x, pb[q].y)));
-                } else {  // L = 1: the reference's (0.0 + term)
-                    pa[q] = cmul_bk<false>(x, ka);
-                    pb[q] = cmul_bk<false>(x, kb);
-                }
-            }
-        }
-        // hand-off: wave h keeps output h; the partner's rows contribute their partial
-        // (element-wise selects: a select of the arrays themselves goes through scratch)
-        C2 keep[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            s_xp[t + 64 * q] = c2(h ? pa[q].x : pb[q].x, h ? pa[q].y : pb[q].y);
-            keep[q] = c2(h ? pb[q].x : pa[q].x, h ? pb[q].y : pa[q].y);
-        }
-        __syncthreads();  // both partials published
-        C2 e[1][8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const C2 o = s_x[t + 64 * br3(q)];
-            const C2 mine = keep[br3(q)];
-            const C2 lo = c2(h ? o.x : mine.x, h ? o.y : mine.y), hi = c2(h ? mine.x : o.x, h ? mine.y : o.y);
-            e[0][q] = c2(lo.x + hi.x, lo.y + hi.y);  // rows 0..L-1 first, then rows L..2L-1
-        }
-        fft512<1, true, FU>(e, s_x, T, t);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            double re, im;
-            untwist_out<false, FU>(e[0][q], twist_t[64 * q], re, im);
-            acc[q] += to_torus<SMALL, FU>(re, near);
-            acc[q + 8] += to_torus<SMALL, FU>(im, near);
-        }
-    }
-
-    if (FU) near_tie_flag(P, near, g, valid);
-    // epilogue through this wave's buffer: acc_h at [0, 1024)
-#pragma unroll
-    for (int m = 0; m < 16; m++) s_xw[t + 64 * m] = acc[m];
-    wave_sync();
-    if (!valid) return;
-    if (out_mode == BR_OUT_LV1) {  // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j], p[N] = b[0]
-        uint32_t *o = out + g * (size_t)1025;
-        if (h == 0) {
-            for (int j = t; j < 1024; j += 64) o[j] = j == 0 ? s_xw[0] : 0u - s_xw[1024 - j];
-        } else if (t == 0) {
-            o[1024] = s_xw[0];
-        }
-    } else if (out_mode == BR_OUT_LV0_EXTRACT2) {  // sampleExtractIndex2 (trlwe.zig:165-180)
-        uint32_t *o = out + g * (size_t)(n + 1);
-        if (h == 0) {
-            for (int j = t; j < n; j += 64) o[j] = j == 0 ? s_xw[0] : 0u - s_xw[n - j];
-        } else if (t == 0) {
-            o[n] = s_xw[0];
-        }
-    } else {
-        uint32_t *o = out + g * (size_t)2048 + h * 1024;
-        for (int j = t; j < 1024; j += 64) o[j] = s_xw[j];
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -3920,29 +3519,6 @@ hipError_t launch_tlwe_gather(const KParams &P, const uint32_t *src, const uint3
 
 // The pair form: fused (exact-integer regime) for any L, the reference's trees
 // only for L = 1 (where its regrouped sum is the reference's order).
-template <int L, bool SMALL>
-static bool launch_pair(const KParams &P, const DevTables &T, const uint8_t *ops, const uint32_t *in_a,
-                        const uint32_t *in_b, const uint32_t *idx, const uint32_t *testvec, const double2 *bk2,
-                        uint32_t *out, int out_mode, size_t B, hipStream_t s, bool fused, const char **used) {
-    const dim3 grid((unsigned)((B + BP_GATES - 1) / BP_GATES)), block(64 * BP_WAVES);
-    if constexpr (SMALL) {
-        if (fused) {
-            hipLaunchKernelGGL((k_blind_rotate_pair<L, true, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,
-                               testvec, bk2, out, out_mode, B);
-            if (used) *used = L == 3 ? "k_blind_rotate_pair<3,true,true> (pair form, fused)"
-                              : L == 2 ? "k_blind_rotate_pair<2,true,true> (pair form, fused)"
-                                       : "k_blind_rotate_pair<1,true,true> (pair form, fused)";
-            return true;
-        }
-    }
-    if constexpr (L == 1) {
-        hipLaunchKernelGGL((k_blind_rotate_pair<1, SMALL, false>), grid, block, 0, s, P, T, ops, in_a, in_b, idx,
-                           testvec, bk2, out, out_mode, B);
-        if (used) *used = SMALL ? "k_blind_rotate_pair<1,true,false> (pair form)" : "k_blind_rotate_pair<1,false,false> (pair form)";
-        return true;
-    }
-    return false;
-}
 
 // |external product| <= 2L * N * Bg/2 * 2^31 below 2^49: the SMALL conversions
 // and the fused arithmetic's guarded conversion hold (the L=3 / Bg=2^6 sets:
@@ -3974,11 +3550,10 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     if (B == 0) return hipSuccess;
     const double2 *bk2 = reinterpret_cast<const double2 *>(bkd);
     const bool small = small_products(P);
-    // form: 'W' latency (8 waves per item), 's' split (2 waves per item),
+    // form: 'W' latency (8 waves per item),
     // 'w' whole (1 wave per item; loader waves unless LaunchOpts::br_loader = 0)
-    const bool split = form == 's';
     const bool wide = form == 'W';
-    const bool loader = !wide && !split && O.br_loader != 0;
+    const bool loader = !wide && O.br_loader != 0;
     // fused arithmetic in the exact-integer regime (SMALL) unless the
     // reference expression trees are requested (TFHE_OPT_ARITH)
     const bool fused = small && fused_allowed(O);
@@ -4026,26 +3601,10 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
         if (ok) return hipGetLastError();
         form = 'w';
     }
-    if (form == 'p') {  // pair form (2 waves per item); falls back to the whole form where not exact
-        bool ok = false;
-        switch (P.L) {
-        case 1: ok = small ? launch_pair<1, true>(P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, fused, used)
-                           : launch_pair<1, false>(P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, fused, used);
-                break;
-        case 2: ok = small && launch_pair<2, true>(P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, fused, used); break;
-        case 3: ok = small && launch_pair<3, true>(P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, fused, used); break;
-        default: break;
-        }
-        if (ok) return hipGetLastError();
-        form = 'w';
-    }
     dim3 grid, block;
     if (wide) {
         grid = dim3((unsigned)B);
         block = dim3(64 * BW_WAVES);
-    } else if (split) {
-        grid = dim3((unsigned)((B + BS_GATES - 1) / BS_GATES));
-        block = dim3(64 * BS_WAVES);
     } else {
         grid = dim3((unsigned)((B + BR_WAVES - 1) / BR_WAVES));
         block = dim3(64 * BR_WAVES * (loader ? 2 : 1));
@@ -4070,14 +3629,6 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
             hipLaunchKernelGGL((k_blind_rotate_wide<L_, S_, false>), grid, block, 0, s, P, T, ops, in_a, in_b,    \
                                idx, testvec, bk2, out, out_mode, B);                                              \
             if (used) *used = "k_blind_rotate_wide<" #L_ "," #S_ ",false> (latency form)";                        \
-        } else if (split && fused) {                                                                              \
-            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_, S_>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, \
-                               testvec, bk2, out, out_mode, B);                                                   \
-            if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ ",true> (split form, fused)";                   \
-        } else if (split) {                                                                                       \
-            hipLaunchKernelGGL((k_blind_rotate_split<L_, S_, false>), grid, block, 0, s, P, T, ops, in_a, in_b,   \
-                               idx, testvec, bk2, out, out_mode, B);                                              \
-            if (used) *used = "k_blind_rotate_split<" #L_ "," #S_ ",false> (split form)";                         \
         } else if (loader && fused && O.br_flags) {                                                               \
             WHOLE_DEFAULT_LAUNCH(L_, S_);                                                                         \
             if (used) *used = "k_blind_rotate<" #L_ "," #S_ ",true,true,true> (whole form, loader waves, slot counters, fused)"; \
@@ -4197,8 +3748,7 @@ static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T
                                             const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
                                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (O.br_form) {  // forced form (TFHE_OPT_BR_FORM): the whole batch in one launch
-        const char f = O.br_form == 2 ? 's' : O.br_form == 3 || O.br_form == 7 ? 'W' : O.br_form == 4 ? 'p'
-                     : O.br_form == 5 ? 'o' : O.br_form == 6 ? 'd' : 'w';
+        const char f = O.br_form == 3 || O.br_form == 7 ? 'W' : O.br_form == 5 ? 'o' : O.br_form == 6 ? 'd' : 'w';
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
     const size_t round = BR_WAVES * device_cus(), tail = B % round;

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "94fc3d60340ab112"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "a40108a8a968a632"; }

@@ -31,7 +31,7 @@ OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 3, "ks_narrow": 0, "
                    "host_pipeline": 0, "circuit_split": 0}
 # status codes (include/tfhe_gpu.h TFHE_ERR_*)
 ERR_INVALID, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_IO, ERR_DEVICE = -1, -2, -3, -4, -5, -6
-BR_FORMS = {"auto": 0, "whole": 1, "split": 2, "wide": 3, "pair": 4, "octo": 5, "duo": 6, "wide2": 7}
+BR_FORMS = {"auto": 0, "whole": 1, "wide": 3, "octo": 5, "duo": 6, "wide2": 7}  # 2 split, 4 pair: removed (round 4)
 TWIDDLES_GLIBC, TWIDDLES_FDLIBM = 0, 1
 ARITH_AUTO, ARITH_REFERENCE, ARITH_FUSED_FORCED = 0, 1, 2
 
