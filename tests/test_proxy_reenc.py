@@ -213,6 +213,35 @@ def test_gpu_reencrypt_gemm_and_lanes_agree(oracle, P, keys, reenc_ab):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ks_form", [3, 0])
+def test_gpu_reencrypt_device_resident(oracle, P, keys, reenc_ab, ks_form):
+    """tfhe_gpu_reencrypt_batch_dev (device buffers, async on the context stream):
+    the host-buffer call's words for ragged batches, in both key-switch forms,
+    with the input buffer sized exactly (the GEMM's whole-block reads go through
+    the staging copy's slack), and the oracle on samples."""
+    import torch
+    ctx = tfhe_amd.Context(N128, device=0)
+    hr = tfhe_amd.HipReencryptor(ctx, tfhe_amd.ProxyReencryptionKey(reenc_ab, P.basebit, P.iks_t))
+    try:
+        with ctx.options(ks_form=ks_form):
+            for B in (1, 65, 1500):
+                x = _random_cts(P, B, 300 + B)
+                want = hr.reencrypt(x)
+                t_in = torch.from_numpy(x.view(np.int32)).to("cuda:0")
+                t_out = torch.zeros_like(t_in)
+                ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+                hr.reencrypt_dev(t_in.data_ptr(), t_out.data_ptr(), B)
+                ctx.sync()
+                got = t_out.cpu().numpy().view(np.uint32)
+                assert np.array_equal(got, want), B
+                assert np.array_equal(got[B - 1], oracle.reencrypt(P.n, P.basebit, P.iks_t, x[B - 1], reenc_ab))
+    finally:
+        ctx.set_stream(0)
+        hr.close()
+        ctx.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pname,basebit,t", [("80", 2, 7), ("128", 4, 4), ("uint4", 5, 3)])
 def test_gpu_reencrypt_other_bases(oracle, pname, basebit, t):
     from oracle import params

@@ -1203,6 +1203,32 @@ static int reencrypt_batch_one(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, con
     return d2h_sync(c, out, c->s_out.p, B * w * 4);
 }
 
+// Device-resident re-encryption (async on the context stream, like the other
+// _dev entry points): the input is copied device-to-device into the staging
+// buffer, whose slack the GEMM form's whole-block reads need; the kernel writes
+// out_dev directly.
+static int reencrypt_batch_dev_one(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const uint32_t *in_dev,
+                                   uint32_t *out_dev, size_t B) {
+    if (!c || !k || (B && (!in_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (k->device != c->device) return fail(c, TFHE_ERR_INVALID, "key belongs to another device");
+    if (B == 0) return TFHE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t w = tlwe0_words(c);
+    int rc = ensure(c, c->s_a, B * w * 4 + KS_GEMM_INPUT_SLACK);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->s_a.p, in_dev, B * w * 4, hipMemcpyDeviceToDevice, c->stream));
+    KsGemm G;
+    if (k->d_key_gemm) {
+        rc = ensure(c, c->s_kspart, ks_gemm_part_bytes(c->K, B, (int)c->P.n, (int)k->basebit));
+        if (rc) return rc;
+        G.kg = k->d_key_gemm;
+        G.part = (uint32_t *)c->s_kspart.p;
+    }
+    HIPCHK(c, launch_reencrypt(c->K, (int)k->t, (int)k->basebit, (const uint32_t *)c->s_a.p, k->d_key, out_dev, B,
+                               c->stream, c->opts, &c->last_ks, &G));
+    return TFHE_OK;
+}
+
 int tfhe_secret_key_new(const tfhe_params *p, uint64_t seed, uint32_t *key_lv0, uint32_t *key_lv1) {
     if (!p || !key_lv0 || !key_lv1) return TFHE_ERR_INVALID;
     host::Rng r(seed);  // SecretKey.new (key.zig:41-57)
@@ -2385,6 +2411,12 @@ int tfhe_gpu_reencrypt_batch(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const
         while (c->shards[d] != s) d++;
         return reencrypt_batch_one(s, d ? k->peers[d - 1] : k, in + b0 * w, out + b0 * w, n);
     });
+}
+
+int tfhe_gpu_reencrypt_batch_dev(tfhe_gpu_ctx *c, const tfhe_gpu_reenc_key *k, const uint32_t *in_dev,
+                                 uint32_t *out_dev, size_t B) {
+    if (is_multi(c)) return fail(c, TFHE_ERR_INVALID, "device-resident calls take a single-device context");
+    return reencrypt_batch_dev_one(c, k, in_dev, out_dev, B);
 }
 
 int tfhe_circuit_partition(size_t n_inputs, size_t n_gates, const uint8_t *ops, const uint32_t *in_a,

@@ -140,6 +140,7 @@ _SIGS = {
     "tfhe_gpu_reenc_key_load": (C.c_int, [vp, u32p, C.c_size_t, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
     "tfhe_gpu_reenc_key_destroy": (None, [vp]),
     "tfhe_gpu_reencrypt_batch": (C.c_int, [vp, vp, u32p, u32p, C.c_size_t]),
+    "tfhe_gpu_reencrypt_batch_dev": (C.c_int, [vp, vp, vp, vp, C.c_size_t]),
     "tfhe_public_key_gen": (C.c_int, [C.POINTER(TfheParams), u32p, C.c_size_t, C.c_double, C.c_uint64, u32p]),
     "tfhe_public_key_encrypt_bool_batch": (C.c_int, [C.POINTER(TfheParams), u32p, C.c_size_t, u8p, C.c_double,
                                                      C.c_uint64, u32p, C.c_size_t]),
@@ -649,6 +650,11 @@ class HipReencryptor:
         self.ctx.check(self.ctx.lib.tfhe_gpu_reencrypt_batch(self.ctx.h, self.h, xp, out.ctypes.data_as(u32p),
                                                              x.shape[0]), "reencrypt")
         return out
+
+    def reencrypt_dev(self, in_ptr, out_ptr, B):
+        """Device-resident batch (async on the context stream): B TLWELv0 at in_ptr -> out_ptr."""
+        self.ctx.check(self.ctx.lib.tfhe_gpu_reencrypt_batch_dev(self.ctx.h, self.h, vp(in_ptr), vp(out_ptr), B),
+                       "reencrypt_dev")
 
 
 class bit_utils:
