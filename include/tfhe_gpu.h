@@ -328,6 +328,10 @@ int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *ctx, const uint8_t *ops_dev, const uin
                             const uint32_t *b_dev, uint32_t *out_dev, size_t B);
 int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *ctx, const uint32_t *in_dev, uint32_t *out_dev,
                                  size_t B);
+/* tfhe_gpu_bootstrap_lut_batch on device buffers (the test vector too: 2N
+ * words of a TRLWE), single-device contexts. */
+int tfhe_gpu_bootstrap_lut_batch_dev(tfhe_gpu_ctx *ctx, const uint32_t *in_dev, const uint32_t *testvec_dev,
+                                     uint32_t *out_dev, size_t B);
 /* tfhe_gpu_reencrypt_batch on device buffers (B TLWELv0 of n + 1 words each),
  * single-device contexts; replaces the same reencryptTLWELv0 loop
  * (proxy_reenc.zig:267-306) without the PCIe copies. */

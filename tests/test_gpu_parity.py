@@ -311,6 +311,35 @@ def test_lut_pbs_uint4(oracle):
     assert np.array_equal(sk.decrypt_lwe_message(out, 16), (msgs + 1) % 16)
 
 
+@pytest.mark.parametrize("pname,B", [("uint4", 4096), ("uint4", 33), ("128", 1500)])
+def test_lut_device_resident(oracle, pname, B):
+    """tfhe_gpu_bootstrap_lut_batch_dev (device buffers, test vector on the device,
+    async on the context stream): the host-buffer call's words (config 5's full
+    4,096 items on the octo form, a ragged batch, and a 128-bit LUT), the oracle
+    on a sample."""
+    import torch
+    c, k = ctx_for(oracle, pname)
+    m = 16 if pname == "uint4" else 4
+    tv = tfhe_amd.lut_generate(c.params, m, lambda x: (3 * x + 1) % m)
+    sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
+    msgs = (np.arange(B) % m).astype(np.uint32)
+    cts = sk.encrypt_lwe_message(msgs, m, seed0=4040 + B)
+    want = c.bootstrap_lut_batch(cts, tv)
+    t_in = torch.from_numpy(np.ascontiguousarray(cts).view(np.int32)).to("cuda:0")
+    t_tv = torch.from_numpy(np.ascontiguousarray(tv, np.uint32).view(np.int32)).to("cuda:0")
+    t_out = torch.zeros_like(t_in)
+    try:
+        c.set_stream(torch.cuda.current_stream().cuda_stream)
+        c.bootstrap_lut_batch_dev(t_in.data_ptr(), t_tv.data_ptr(), t_out.data_ptr(), B)
+        c.sync()
+    finally:
+        c.set_stream(0)
+    got = t_out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    one = oracle.gate_batch(k.p, np.array([255], np.uint8), cts[B - 1][None], cts[B - 1][None], k.ck, testvec=tv)[0]
+    assert np.array_equal(got[B - 1], one)
+
+
 def test_lut_uint4_on_a_key_with_the_reference_noise_constants(oracle):
     """the reference draws every KSK with KSK_ALPHA = 2e-5 and
     every BSK with BSK_ALPHA = 2e-8, the 128-bit constants, for all sets

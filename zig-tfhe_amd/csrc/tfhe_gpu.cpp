@@ -1525,6 +1525,14 @@ int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *c, const uint32_t *in_dev, uint32
     return run_bootstrap_dev(c, nullptr, in_dev, nullptr, nullptr, out_dev, B, RUN_BOOTSTRAP);
 }
 
+int tfhe_gpu_bootstrap_lut_batch_dev(tfhe_gpu_ctx *c, const uint32_t *in_dev, const uint32_t *testvec_dev,
+                                     uint32_t *out_dev, size_t B) {
+    if (!c || !testvec_dev || (B && (!in_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
+    return run_bootstrap_dev(c, nullptr, in_dev, nullptr, testvec_dev, out_dev, B, RUN_BOOTSTRAP);
+}
+
 int tfhe_gpu_profile_begin(tfhe_gpu_ctx *c) {
     if (!c) return TFHE_ERR_INVALID;
     c->profiling = true;

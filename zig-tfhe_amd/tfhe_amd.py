@@ -141,6 +141,7 @@ _SIGS = {
     "tfhe_gpu_reenc_key_destroy": (None, [vp]),
     "tfhe_gpu_reencrypt_batch": (C.c_int, [vp, vp, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_reencrypt_batch_dev": (C.c_int, [vp, vp, vp, vp, C.c_size_t]),
+    "tfhe_gpu_bootstrap_lut_batch_dev": (C.c_int, [vp, vp, vp, vp, C.c_size_t]),
     "tfhe_public_key_gen": (C.c_int, [C.POINTER(TfheParams), u32p, C.c_size_t, C.c_double, C.c_uint64, u32p]),
     "tfhe_public_key_encrypt_bool_batch": (C.c_int, [C.POINTER(TfheParams), u32p, C.c_size_t, u8p, C.c_double,
                                                      C.c_uint64, u32p, C.c_size_t]),
@@ -459,6 +460,10 @@ class Context:
 
     def bootstrap_batch_dev(self, in_ptr, out_ptr, B):
         self.check(self.lib.tfhe_gpu_bootstrap_batch_dev(self.h, vp(in_ptr), vp(out_ptr), B), "bootstrap_batch_dev")
+
+    def bootstrap_lut_batch_dev(self, in_ptr, tv_ptr, out_ptr, B):
+        self.check(self.lib.tfhe_gpu_bootstrap_lut_batch_dev(self.h, vp(in_ptr), vp(tv_ptr), vp(out_ptr), B),
+                   "bootstrap_lut_batch_dev")
 
     # ---- stage entry points
     def fft_forward(self, polys):
