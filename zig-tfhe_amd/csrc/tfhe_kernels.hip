@@ -697,12 +697,18 @@ DEV void mac_row(C2 *fa, C2 *fb, const C2 *d, const double2 *bk, int t) {
 // scheduling fence per group keeps hipcc from hoisting all 32 reads (128
 // VGPRs) ahead of the arithmetic, which pushes the kernel into AGPR copies.
 template <bool FU = false>
-DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 *bk, int t) {
+DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 *bk, int t,
+                      const double2 *k0 = nullptr) {
     double2 k[2][4];
-    k[0][0] = bk[t];
-    k[0][1] = bk[64 + t];
-    k[0][2] = bk[1024 + t];
-    k[0][3] = bk[1024 + 64 + t];
+    if (k0) {  // group 0 already read (TFHE_OPT_PUB: with the slot counter)
+#pragma unroll
+        for (int e = 0; e < 4; e++) k[0][e] = k0[e];
+    } else {
+        k[0][0] = bk[t];
+        k[0][1] = bk[64 + t];
+        k[0][2] = bk[1024 + t];
+        k[0][3] = bk[1024 + 64 + t];
+    }
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         const int c = q & 1;
@@ -1032,6 +1038,9 @@ DEV void issue_bk_pair_async(const double2 *__restrict__ src, double2 *slot, int
     }
 }
 
+#ifndef TFHE_OPT_PUB  // A/B: 1 = the slot counter read in one LDS batch with the MAC's first BK words
+#define TFHE_OPT_PUB 1
+#endif
 template <int L, bool LOADER, bool FU = false, bool FLAGS = false>
 DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *twist_t, C2 *xb, int t, int tid,
                   C2 *fa, C2 *fb, double2 *s_bk, int slot0, const double2 *__restrict__ next_pair, bool has_next,
@@ -1058,6 +1067,8 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #pragma unroll PAIR_UNROLL
     for (int rp = 0; rp < L; rp++) {
         C2 d[2][8];
+        double2 kpre[4];
+        bool pre = false;
         pp.mark(1);
 #ifndef TFHE_PAIR0_LDS
         if (PAIR_UNROLL == L && LOADER && L > 1 && rp == 0)  // UINT4 (L = 1): 1.4 % slower, LDS kept
@@ -1075,7 +1086,47 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
         const int slot = (slot0 + rp) & 1;
         if (FLAGS) {  // pair k = k0 + rp is use (k >> 1) of slot k & 1: wait until all 4 loaders published it
             const uint32_t k = k0 + (uint32_t)rp;
-#ifndef TFHE_KO_WAIT  // knock-out timing build: no wait for the pair's publication (wrong words possible)
+#if TFHE_OPT_PUB
+            // optimistic: the slot counter and the MAC's first BK words in one LDS batch.
+            // A wave's LDS operations execute in order, so words read after a counter
+            // value that says "published" are the published ones; rarely (0.19 per
+            // step, profiles/r04_spin_stats.txt) the pair is not in yet: sleep, read
+            // both again.  One asm loop, so hipcc sees four plain 16-B results.
+            {
+                typedef __attribute__((ext_vector_type(4))) unsigned int u4;
+                u4 q0, q1, q2, q3;
+                uint32_t v, sv, cnt = fail ? 1u : spin_cap;
+                const uint32_t caddr = (uint32_t)(size_t)(lds_void_t *)(sync + (k & 1));
+                const uint32_t baddr = (uint32_t)(size_t)(lds_void_t *)(s_bk + slot * 2048 + t);
+                const uint32_t target = 4u * ((k >> 1) + 1u);
+                asm volatile(
+                    "1:\n\t"
+                    "ds_read_b32 %[v], %[ca]\n\t"
+                    "ds_read_b128 %[q0], %[ba]\n\t"
+                    "ds_read_b128 %[q1], %[ba] offset:1024\n\t"
+                    "ds_read_b128 %[q2], %[ba] offset:16384\n\t"
+                    "ds_read_b128 %[q3], %[ba] offset:17408\n\t"
+                    "s_waitcnt lgkmcnt(0)\n\t"
+                    "v_readfirstlane_b32 %[sv], %[v]\n\t"
+                    "s_cmp_ge_u32 %[sv], %[tgt]\n\t"
+                    "s_cbranch_scc1 2f\n\t"
+                    "s_sleep 1\n\t"
+                    "s_sub_u32 %[cnt], %[cnt], 1\n\t"
+                    "s_cmp_eq_u32 %[cnt], 0\n\t"
+                    "s_cbranch_scc0 1b\n\t"
+                    "s_mov_b32 %[fail], 1\n"
+                    "2:"
+                    : [v] "=&v"(v), [q0] "=&v"(q0), [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), [sv] "=&s"(sv),
+                      [cnt] "+s"(cnt), [fail] "+s"(fail)
+                    : [ca] "v"(caddr), [ba] "v"(baddr), [tgt] "s"(target)
+                    : "memory", "scc");
+                kpre[0] = __builtin_bit_cast(double2, q0);
+                kpre[1] = __builtin_bit_cast(double2, q1);
+                kpre[2] = __builtin_bit_cast(double2, q2);
+                kpre[3] = __builtin_bit_cast(double2, q3);
+                pre = true;
+            }
+#elif !defined(TFHE_KO_WAIT)  // knock-out timing build: no wait for the pair's publication (wrong words possible)
 #ifdef TFHE_SPIN_STATS
             spin_until_ge(sync + (k & 1), 4u * ((k >> 1) + 1u), spin_cap, fail, &pp.spins);
 #else
@@ -1098,7 +1149,7 @@ DEV void br_pairs(const uint32_t *s_tmp, int bgbit, const LdsTw &T, const C2 *tw
 #endif
         pp.mark(3);
 #ifndef TFHE_KO_MAC
-        mac_pair_lds<FU>(fa, fb, d[0], d[1], s_bk + slot * 2048, t);
+        mac_pair_lds<FU>(fa, fb, d[0], d[1], s_bk + slot * 2048, t, pre ? kpre : nullptr);
 #else
         for (int q = 0; q < 8; q++) fa[q] = c2(fa[q].x + d[0][q].x, fa[q].y + d[1][q].y);
 #endif

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "a40108a8a968a632"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "029107cca9f90f89"; }
