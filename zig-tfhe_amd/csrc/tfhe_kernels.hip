@@ -740,6 +740,9 @@ DEV void mac_pair_lds(C2 *fa, C2 *fb, const C2 *d0, const C2 *d1, const double2 
 
 // Inverse transforms of the two accumulated spectra (fft1024 x2) and the
 // CMUX add acc' = ExtProd + acc (trgsw.zig:277-281), lane-local.
+#ifndef TFHE_UNTWIST_EARLY
+#define TFHE_UNTWIST_EARLY 0
+#endif
 template <bool SMALL, int TS, bool ONEBUF = false, bool FU = false, class TW>
 DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const C2 *tws, int t,
                          uint32_t *accA, uint32_t *accB, uint32_t &near) {
@@ -749,6 +752,11 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
         e[0][q] = fa[br3(q)];
         e[1][q] = fb[br3(q)];
     }
+#if TFHE_UNTWIST_EARLY  // A/B: the untwist factors read before the transforms (their latency hidden)
+    C2 wq[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) wq[q] = tws[q * TS];
+#endif
 #ifndef TFHE_KO_INV
     fft512_x2<true, ONEBUF, FU>(e, xb, T, t);
 #endif
@@ -760,7 +768,11 @@ DEV void inverse_and_add(const C2 *fa, const C2 *fb, C2 *xb, const TW &T, const 
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         double ra, ia, rb, ib;
+#if TFHE_UNTWIST_EARLY
+        const C2 w = wq[q];
+#else
         const C2 w = tws[q * TS];
+#endif
         untwist_out<false, FU>(e[0][q], w, ra, ia);
         untwist_out<false, FU>(e[1][q], w, rb, ib);
         accA[q] += to_torus<SMALL, FU>(ra, nq[0]);
