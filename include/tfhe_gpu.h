@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 4
+#define TFHE_GPU_ABI_VERSION 5  /* 5: _dev LUT / re-encryption entries; BR forms 2 and 4 removed */
 
 enum {
     TFHE_OK = 0,
