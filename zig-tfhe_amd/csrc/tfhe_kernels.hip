@@ -1912,7 +1912,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
     C2 *s_xp = reinterpret_cast<C2 *>(bufs + pw * BD_LDS_BUF);  // partner's buffer (hand-off target)
     uint16_t *s_at = reinterpret_cast<uint16_t *>(bufs + BD_WAVES * BD_LDS_BUF + gs * BD_LDS_AT);
     uint32_t *s_sync = reinterpret_cast<uint32_t *>(smem + BD_LDS_TOTAL - BD_LDS_SYNC);
-    uint32_t *s_pub = s_sync, *s_done = s_sync + 2, *s_fwd = s_sync + 4, *s_hand = s_sync + 12, *s_cl = s_sync + 24;
+    uint32_t *s_pub = s_sync, *s_done = s_sync + 2, *s_fwd = s_sync + 4, *s_hand = s_sync + 12;
+#if TFHE_DUO_PROTO == 1
+    uint32_t *s_cl = s_sync + 24;  // the next unclaimed level
+#endif
     int *s_bt = reinterpret_cast<int *>(s_sync + 20);
 
     if (lds_layout_bad(smem)) {
