@@ -275,6 +275,21 @@ def timed(fn, steps, warmup, world, device):
     return el, out
 
 
+def timed_circuit(ctx, circ, inputs, args, world, device):
+    """A circuit workload timed both ways: through host buffers (tfhe_gpu_circuit_eval, PCIe
+    copies in the timed region) and on HBM-resident inputs and outputs
+    (tfhe_gpu_circuit_eval_dev on the torch stream: the line's value).
+    -> (elapsed dev, outputs dev, depth, elapsed host, outputs host)."""
+    el_host, (outs_host, depth) = timed(lambda: circ.run(ctx, inputs), args.steps, args.warmup, world, device)
+    t_in = torch.from_numpy(np.ascontiguousarray(inputs).view(np.int32)).to(device)
+    t_out = torch.zeros((len(circ.outputs), inputs.shape[1]), dtype=torch.int32, device=device)
+    ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+    el, _ = timed(lambda: circ.run_dev(ctx, t_in.data_ptr(), t_out.data_ptr()), args.steps, args.warmup, world, device)
+    outs = t_out.cpu().numpy().view(np.uint32)
+    ctx.set_stream(0)
+    return el, outs, depth, el_host, outs_host
+
+
 def apply_opts(ctx, args):
     """--opt NAME=VALUE -> tfhe_gpu_set_option (names: tfhe_amd.OPTIONS)."""
     for kv in args.opt:
@@ -335,14 +350,17 @@ def run_workload(args, rank, world, device):
         bits = np.concatenate([((xa[:, None] >> np.arange(16)) & 1).ravel(), ((xb[:, None] >> np.arange(16)) & 1).ravel(),
                                np.zeros(nadd, np.int64)]).astype(np.uint8)
         inputs = sk.encrypt_bool(bits, seed0=1)
-        el, (outs, depth) = timed(lambda: c.run(ctx, inputs), args.steps, args.warmup, world, device)
+        el, outs, depth, el_host, outs_host = timed_circuit(ctx, c, inputs, args, world, device)
         dec = sk.decrypt_bool(outs).reshape(nadd, 16)
         vals = (dec.astype(np.int64) << np.arange(16)).sum(1)
-        ok = bool(np.array_equal(vals, (xa + xb) & 0xFFFF)) and int(vals[0]) == 706
+        ok = bool(np.array_equal(vals, (xa + xb) & 0xFFFF)) and int(vals[0]) == 706 and \
+            bool(np.array_equal(outs, outs_host))
         units = len(c.ops) * world * args.steps  # every adder gate is a bootstrap
         metric, unit = "gate-bootstraps/sec (16-bit ripple-carry adders, level-scheduled circuit)", "gate-bootstraps/s"
         extra = {"adders_per_step": nadd * world, "gates_per_adder": len(c.ops) // nadd, "levels": depth,
-                 "ms_per_adder_circuit": round(el / args.steps * 1e3, 3), "sums_check": ok}
+                 "ms_per_adder_circuit": round(el / args.steps * 1e3, 3), "sums_check": ok,
+                 "host_buffers": {"ms_per_step": round(el_host / args.steps * 1e3, 3),
+                                  "note": "tfhe_gpu_circuit_eval: input/output PCIe copies in the timed region"}}
         workload = f"{nadd} independent 16-bit ripple-carry adders per GPU (examples/add_two_numbers.zig), 402+304 first"
         scaling = "weak"
     elif args.workload == "mixed":
@@ -359,13 +377,16 @@ def run_workload(args, rank, world, device):
             elif kinds[k] == 2: c.output(c.xor(x, y)); want[k] = bx ^ by
             else: c.output(c.mux(x, y, z)); want[k] = by if bx else bz
         inputs = sk.encrypt_bool(bits, seed0=1)
-        el, (outs, depth) = timed(lambda: c.run(ctx, inputs), args.steps, args.warmup, world, device)
-        ok = bool(np.array_equal(sk.decrypt_bool(outs), want))
+        el, outs, depth, el_host, outs_host = timed_circuit(ctx, c, inputs, args, world, device)
+        ok = bool(np.array_equal(sk.decrypt_bool(outs), want)) and bool(np.array_equal(outs, outs_host))
         n_boot = int(sum(1 for op in c.ops if op != tfhe_amd.NOT))
         units = total * args.steps
         metric, unit = "gates/sec (mixed AND/OR/XOR/MUX, 128-bit)", "gates/s"
         extra = {"bootstraps_per_sec": round(n_boot * world * args.steps / el, 2), "levels": depth,
-                 "decrypt_check": ok, "round_packing": not args.no_pack}
+                 "decrypt_check": ok, "round_packing": not args.no_pack,
+                 "host_buffers": {"value": round(total * args.steps / el_host, 2),
+                                  "ms_per_step": round(el_host / args.steps * 1e3, 3),
+                                  "note": "tfhe_gpu_circuit_eval: input/output PCIe copies in the timed region"}}
         workload = (f"{total} gates over {world} GPU(s) ({B} on rank 0), op uniform over AND/OR/XOR/MUX "
                     f"(MUX = 3 bootstraps, 2 levels)")
     elif args.workload == "reenc":

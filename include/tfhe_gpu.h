@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 5  /* 5: _dev LUT / re-encryption entries; BR forms 2 and 4 removed */
+#define TFHE_GPU_ABI_VERSION 5  /* 5: _dev LUT / re-encryption / circuit entries; BR forms 2 and 4 removed */
 
 enum {
     TFHE_OK = 0,
@@ -297,6 +297,12 @@ int tfhe_gpu_bootstrap_lut_batch(tfhe_gpu_ctx *ctx, const uint32_t *in, const ui
 int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
                           const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
                           const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels);
+/* The same with the inputs and outputs in HBM (the circuit itself, ops / in_a /
+ * in_b / out_wires, stays a host description), single-device contexts, async on
+ * the context stream (tfhe_gpu_sync reports device errors). */
+int tfhe_gpu_circuit_eval_dev(tfhe_gpu_ctx *ctx, size_t n_inputs, const uint32_t *inputs_dev, size_t n_gates,
+                              const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
+                              const uint32_t *out_wires, uint32_t *outputs_dev, uint32_t *levels);
 
 /* The schedule tfhe_gpu_circuit_eval runs, host only (no device): levels[g]
  * = the level gate g runs at (NOT: the level of its input), *depth (may be

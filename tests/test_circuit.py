@@ -96,6 +96,52 @@ def test_circuit_mixed_gates_with_mux(oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["adder128", "wide80"])
+def test_circuit_device_resident(oracle, shape):
+    """tfhe_gpu_circuit_eval_dev (inputs and outputs in HBM, async on the context
+    stream) returns the host-buffer call's words and depth: the 16-bit adder at
+    128-bit (33 levels), and a 2-level 80-bit circuit of 1,030 gates per level
+    (a whole-form round plus a tail round)."""
+    import torch
+    from conftest import get_keys
+    pname = "128" if shape == "adder128" else "80"
+    k = get_keys(oracle, pname)
+    ctx = tfhe_amd.Context(pname, 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    sk = tfhe_amd.SecretKey(ctx.params, k.k0, k.k1)
+    c = Circuit()
+    if shape == "adder128":
+        A = [c.input() for _ in range(16)]
+        Bw = [c.input() for _ in range(16)]
+        cin = c.input()
+        s, carry = c.ripple_add(A, Bw, cin)
+        c.output(*s, carry)
+        bits = [(402 >> i) & 1 for i in range(16)] + [(304 >> i) & 1 for i in range(16)] + [0]
+    else:
+        ins = [c.input() for _ in range(40)]
+        g = np.random.default_rng(11)
+        first = [c.nand(ins[int(x)], ins[int(y)]) for x, y in g.integers(0, 40, (1030, 2))]
+        for i in range(1030):
+            c.output(c.xor(first[i], first[(i * 7 + 3) % 1030]))
+        bits = g.integers(0, 2, 40).tolist()
+    inputs = sk.encrypt_bool(bits, seed0=91)
+    want, depth = c.run(ctx, inputs)
+    t_in = torch.from_numpy(np.ascontiguousarray(inputs).view(np.int32)).to("cuda:0")
+    t_out = torch.full((len(c.outputs), inputs.shape[1]), -1, dtype=torch.int32, device="cuda:0")
+    try:
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        d2 = c.run_dev(ctx, t_in.data_ptr(), t_out.data_ptr())
+        ctx.sync()
+    finally:
+        ctx.set_stream(0)
+    assert d2 == depth
+    assert np.array_equal(t_out.cpu().numpy().view(np.uint32), want)
+    if shape == "adder128":
+        assert sum(int(x) << i for i, x in enumerate(sk.decrypt_bool(want[:16]))) == 706
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_circuit_rejects_bad_graphs(oracle):
     from conftest import get_keys
     k = get_keys(oracle, "80")

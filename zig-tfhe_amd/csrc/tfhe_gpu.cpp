@@ -1443,7 +1443,7 @@ const char *plan_circuit(size_t n_inputs, size_t n_gates, const uint8_t *ops, co
 // Device side of a plan on one context: wire table with the inputs, the gather
 // indices and op codes, uploaded on its stream.
 int upload_plan(tfhe_gpu_ctx *c, const CircuitPlan &pl, size_t W, size_t n_inputs, const uint32_t *inputs,
-                size_t n_outputs) {
+                size_t n_outputs, bool inputs_on_device = false) {
     const size_t w1 = tlwe0_words(c);
     HIPCHK(c, hipSetDevice(c->device));
     int rc = ensure(c, c->s_wires, std::max<size_t>(W, 1) * w1 * 4);
@@ -1451,7 +1451,9 @@ int upload_plan(tfhe_gpu_ctx *c, const CircuitPlan &pl, size_t W, size_t n_input
     if (!rc) rc = ensure(c, c->s_cops, std::max<size_t>(pl.cops.size(), 1));
     if (!rc) rc = ensure(c, c->s_out, std::max<size_t>(n_outputs, 1) * w1 * 4);
     if (rc) return rc;
-    if (n_inputs) HIPCHK(c, hipMemcpyAsync(c->s_wires.p, inputs, n_inputs * w1 * 4, hipMemcpyHostToDevice, c->stream));
+    if (n_inputs)
+        HIPCHK(c, hipMemcpyAsync(c->s_wires.p, inputs, n_inputs * w1 * 4,
+                                 inputs_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
     if (!pl.idx.empty())
         HIPCHK(c, hipMemcpyAsync(c->s_cidx.p, pl.idx.data(), pl.idx.size() * 4, hipMemcpyHostToDevice, c->stream));
     if (!pl.cops.empty())
@@ -1463,9 +1465,12 @@ int upload_plan(tfhe_gpu_ctx *c, const CircuitPlan &pl, size_t W, size_t n_input
 
 extern "C" {
 
+// dev: inputs and outputs are device pointers (tfhe_gpu_circuit_eval_dev): the inputs are copied
+// device-to-device into the wire table, the outputs gathered straight into `outputs`, and the call
+// returns without waiting (async on the context stream, like the other _dev entries)
 static int circuit_eval_one(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates,
                           const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
-                          const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels_out) {
+                          const uint32_t *out_wires, uint32_t *outputs, uint32_t *levels_out, bool dev = false) {
     if (!c || (n_inputs && !inputs) || (n_gates && (!ops || !in_a || !in_b)) || (n_outputs && (!out_wires || !outputs)))
         return fail(c, TFHE_ERR_INVALID, "null argument");
     if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
@@ -1475,7 +1480,7 @@ static int circuit_eval_one(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *in
     if (const char *why = plan_circuit(n_inputs, n_gates, ops, in_a, in_b, n_outputs, out_wires, c->circuit_pack != 0,
                                        device_cus(), pl))
         return fail(c, TFHE_ERR_INVALID, why);
-    int rc = upload_plan(c, pl, W, n_inputs, inputs, n_outputs);
+    int rc = upload_plan(c, pl, W, n_inputs, inputs, n_outputs, dev);
     if (rc) return rc;
     const auto &bs = pl.bs;
     const auto &nots = pl.nots;
@@ -1500,10 +1505,13 @@ static int circuit_eval_one(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *in
             sp += nn;
         }
     }
-    if (n_outputs) {
+    if (n_outputs && dev) {
+        HIPCHK(c, launch_tlwe_gather(c->K, wires, d_idx + ip, outputs, n_outputs, false, c->stream));
+    } else if (n_outputs) {
         HIPCHK(c, launch_tlwe_gather(c->K, wires, d_idx + ip, (uint32_t *)c->s_out.p, n_outputs, false, c->stream));
         rc = d2h_sync(c, outputs, c->s_out.p, n_outputs * w1 * 4);
         if (rc) return rc;
+    } else if (dev) {
     } else {
         rc = sync_check(c);
         if (rc) return rc;
@@ -2439,6 +2447,14 @@ int tfhe_circuit_partition(size_t n_inputs, size_t n_gates, const uint8_t *ops, 
     partition_gates(n_inputs, n_gates, ops, in_a, in_b, (size_t)num_devices, dev);
     std::copy(dev.begin(), dev.end(), device_of_gate);
     return TFHE_OK;
+}
+
+int tfhe_gpu_circuit_eval_dev(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs_dev, size_t n_gates,
+                              const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, size_t n_outputs,
+                              const uint32_t *out_wires, uint32_t *outputs_dev, uint32_t *levels) {
+    if (is_multi(c)) return fail(c, TFHE_ERR_INVALID, "device-resident calls take a single-device context");
+    return circuit_eval_one(c, n_inputs, inputs_dev, n_gates, ops, in_a, in_b, n_outputs, out_wires, outputs_dev,
+                            levels, true);
 }
 
 int tfhe_gpu_circuit_eval(tfhe_gpu_ctx *c, size_t n_inputs, const uint32_t *inputs, size_t n_gates, const uint8_t *ops,

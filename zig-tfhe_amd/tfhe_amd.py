@@ -115,6 +115,8 @@ _SIGS = {
     "tfhe_gpu_gate_batch": (C.c_int, [vp, u8p, u32p, u32p, u32p, C.c_size_t]),
     "tfhe_gpu_circuit_eval": (C.c_int, [vp, C.c_size_t, u32p, C.c_size_t, u8p, u32p, u32p, C.c_size_t, u32p, u32p,
                                         C.POINTER(C.c_uint32)]),
+    "tfhe_gpu_circuit_eval_dev": (C.c_int, [vp, C.c_size_t, vp, C.c_size_t, u8p, u32p, u32p, C.c_size_t, u32p, vp,
+                                        C.POINTER(C.c_uint32)]),
     "tfhe_circuit_schedule": (C.c_int, [C.c_size_t, C.c_size_t, u8p, u32p, u32p, C.c_uint32, C.c_int, u32p,
                                         C.POINTER(C.c_uint32)]),
     "tfhe_circuit_partition": (C.c_int, [C.c_size_t, C.c_size_t, u8p, u32p, u32p, C.c_int, u32p]),
@@ -426,6 +428,18 @@ class Context:
                                                   bp, out_wires.size, op_, out.ctypes.data_as(u32p), C.byref(lv)),
                    "circuit_eval")
         return out, lv.value
+
+    def circuit_eval_dev(self, inputs_ptr, n_inputs, ops, in_a, in_b, out_wires, outputs_ptr):
+        """tfhe_gpu_circuit_eval_dev: inputs / outputs in HBM (async on the context stream). -> depth."""
+        ops = np.ascontiguousarray(ops, np.uint8)
+        in_a, ap = _u32(in_a)
+        in_b, bp = _u32(in_b)
+        out_wires, op_ = _u32(out_wires)
+        lv = C.c_uint32()
+        self.check(self.lib.tfhe_gpu_circuit_eval_dev(self.h, n_inputs, vp(inputs_ptr), ops.size, ops.ctypes.data_as(u8p),
+                                                      ap, bp, out_wires.size, op_, vp(outputs_ptr), C.byref(lv)),
+                   "circuit_eval_dev")
+        return lv.value
 
     def gate_batch(self, ops, a, b):
         ops = np.ascontiguousarray(ops, dtype=np.uint8)
@@ -909,3 +923,9 @@ class Circuit:
             raise ValueError(f"circuit has {self.n_inputs} inputs, got {inputs.shape[0]}")
         return ctx.circuit_eval(inputs, np.array(self.ops, np.uint8), np.array(self.ia, np.uint32),
                                 np.array(self.ib, np.uint32), np.array(self.outputs, np.uint32))
+
+    def run_dev(self, ctx: "Context", inputs_ptr, outputs_ptr):
+        """Inputs (n_inputs TLWELv0) and outputs in HBM; returns the bootstrap depth."""
+        return ctx.circuit_eval_dev(inputs_ptr, self.n_inputs, np.array(self.ops, np.uint8),
+                                    np.array(self.ia, np.uint32), np.array(self.ib, np.uint32),
+                                    np.array(self.outputs, np.uint32), outputs_ptr)
