@@ -1454,6 +1454,8 @@ int upload_plan(tfhe_gpu_ctx *c, const CircuitPlan &pl, size_t W, size_t n_input
     if (n_inputs)
         HIPCHK(c, hipMemcpyAsync(c->s_wires.p, inputs, n_inputs * w1 * 4,
                                  inputs_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    // the plan vectors are pageable: hipMemcpyAsync stages them before it returns, so the caller
+    // may drop `pl` while the copies are still in flight (the _dev circuit call does not sync)
     if (!pl.idx.empty())
         HIPCHK(c, hipMemcpyAsync(c->s_cidx.p, pl.idx.data(), pl.idx.size() * 4, hipMemcpyHostToDevice, c->stream));
     if (!pl.cops.empty())
