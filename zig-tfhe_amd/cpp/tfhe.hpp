@@ -433,6 +433,17 @@ class Circuit {
         for (size_t k = 0; k < outs_.size(); k++) std::copy(out.begin() + k * w, out.begin() + (k + 1) * w, r[k].p.begin());
         return r;
     }
+    // Inputs (numInputs() TLWELv0 words, row-major) and outputs (numOutputs()) in HBM;
+    // async on the context stream (tfhe_gpu_circuit_eval_dev). Returns the bootstrap depth.
+    uint32_t runDevice(const CloudKey &ck, const Torus *inputs_dev, Torus *outputs_dev) const {
+        uint32_t levels = 0;
+        check(tfhe_gpu_circuit_eval_dev(ck.ctx(), n_inputs_, inputs_dev, ops_.size(), ops_.data(), ia_.data(),
+                                        ib_.data(), outs_.size(), outs_.data(), outputs_dev, &levels),
+              "Circuit.runDevice", ck.ctx());
+        return levels;
+    }
+    size_t numInputs() const { return n_inputs_; }
+    size_t numOutputs() const { return outs_.size(); }
 
   private:
     uint32_t n_inputs_ = 0;
