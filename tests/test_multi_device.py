@@ -123,6 +123,8 @@ def test_two_shards_circuit_components(oracle):
     assert depth == d1 == 33 and np.array_equal(got, want)
     dec = sk.decrypt_bool(got).reshape(2, 16)
     assert [sum(int(b) << i for i, b in enumerate(row)) for row in dec] == [706, 5555]
+    with pytest.raises(RuntimeError):  # device-resident circuits take a single-device context
+        c.run_dev(multi, 0, 0)
     single.close()
     multi.close()
 
