@@ -142,6 +142,33 @@ def test_circuit_device_resident(oracle, shape):
 
 
 @pytest.mark.gpu
+def test_circuit_device_resident_edges(oracle):
+    """tfhe_gpu_circuit_eval_dev edge cases: no gates (the outputs are the inputs,
+    reordered), no outputs (depth only), a bad graph rejected before any copy."""
+    import torch
+    from conftest import get_keys
+    k = get_keys(oracle, "80")
+    ctx = tfhe_amd.Context("80", 0)
+    ctx.load_cloud_key(k.ck.offset, k.ck.testvec, k.ck.bk, k.ck.ksk)
+    w = ctx.params.n + 1
+    x = np.random.default_rng(3).integers(0, 2**32, (3, w), dtype=np.uint32)
+    t_in = torch.from_numpy(x.view(np.int32)).to("cuda:0")
+    t_out = torch.zeros((3, w), dtype=torch.int32, device="cuda:0")
+    none8, none32 = np.zeros(0, np.uint8), np.zeros(0, np.uint32)
+    assert ctx.circuit_eval_dev(t_in.data_ptr(), 3, none8, none32, none32, np.array([2, 0, 1], np.uint32),
+                                t_out.data_ptr()) == 0
+    ctx.sync()
+    assert np.array_equal(t_out.cpu().numpy().view(np.uint32), x[[2, 0, 1]])
+    assert ctx.circuit_eval_dev(t_in.data_ptr(), 3, np.array([tfhe_amd.NAND], np.uint8), np.array([0], np.uint32),
+                                np.array([1], np.uint32), none32, 0) == 1
+    with pytest.raises(RuntimeError):  # forward reference
+        ctx.circuit_eval_dev(t_in.data_ptr(), 3, np.array([tfhe_amd.AND], np.uint8), np.array([0], np.uint32),
+                             np.array([3], np.uint32), np.array([3], np.uint32), t_out.data_ptr())
+    ctx.sync()
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_circuit_rejects_bad_graphs(oracle):
     from conftest import get_keys
     k = get_keys(oracle, "80")
