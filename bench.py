@@ -230,9 +230,14 @@ def rooflines(p, B, params, br_avg_s, kernel):
     # the same kernel's rocprofv3 --stats average, beside the HIP-event one above
     rp, rwhy = rocprof_record()
     if rp:
-        roof["kernel_avg_ms_rocprof"] = rp["avg_ms"]
-        roof["rocprof"] = {k: rp[k] for k in ("launches", "min_ms", "max_ms", "source") if k in rp}
-        roof["frac_rocprof"] = round(ops / (rp["avg_ms"] / 1e3) / VALU_F64_PEAK, 4)
+        # rocprof basis: the average over the recorded launches without the slowest one (the
+        # first launch of the run, a warm-up: its code-object load and cold caches), reproducible
+        # from the committed csv as (TotalDurationNs - MaxNs) / (Calls - 1)
+        avg = rp.get("avg_ms_without_max", rp["avg_ms"])
+        roof["kernel_avg_ms_rocprof"] = avg
+        roof["rocprof"] = {k: rp[k] for k in ("launches", "avg_ms", "min_ms", "max_ms", "source") if k in rp}
+        roof["rocprof"]["basis"] = "(TotalDurationNs - MaxNs) / (Calls - 1) of the csv row: the warm-up launch excluded"
+        roof["frac_rocprof"] = round(ops / (avg / 1e3) / VALU_F64_PEAK, 4)
     else:
         roof["rocprof_note"] = rwhy
     alg = algorithmic_bytes_per_gate(p) * B
@@ -324,6 +329,25 @@ def shared_secret_key(ctx, p, rank, world, device):
     return sk
 
 
+def mixed_circuit(B, g):
+    """Config 4: B independent gates, op uniform over AND/OR/XOR/MUX (a MUX is
+    3 bootstraps in 2 levels, gates.zig:124-129), each over its own 3 inputs.
+    -> (circuit, input bits, expected output bits)."""
+    c = tfhe_amd.Circuit()
+    ins = [c.input() for _ in range(3 * B)]
+    kinds = g.integers(0, 4, B)
+    bits = g.integers(0, 2, 3 * B).astype(np.uint8)
+    want = np.empty(B, bool)
+    for k in range(B):
+        x, y, z = ins[3 * k], ins[3 * k + 1], ins[3 * k + 2]
+        bx, by, bz = bits[3 * k], bits[3 * k + 1], bits[3 * k + 2]
+        if kinds[k] == 0: c.output(c.and_(x, y)); want[k] = bx & by
+        elif kinds[k] == 1: c.output(c.or_(x, y)); want[k] = bx | by
+        elif kinds[k] == 2: c.output(c.xor(x, y)); want[k] = bx ^ by
+        else: c.output(c.mux(x, y, z)); want[k] = by if bx else bz
+    return c, bits, want
+
+
 def run_workload(args, rank, world, device):
     """Configs 3-5 of BASELINE.json (host-buffer APIs: PCIe copies included)."""
     pname = "uint4" if args.workload == "lut" else args.params
@@ -364,18 +388,7 @@ def run_workload(args, rank, world, device):
         workload = f"{nadd} independent 16-bit ripple-carry adders per GPU (examples/add_two_numbers.zig), 402+304 first"
         scaling = "weak"
     elif args.workload == "mixed":
-        c = tfhe_amd.Circuit()
-        ins = [c.input() for _ in range(3 * B)]
-        kinds = g.integers(0, 4, B)
-        bits = g.integers(0, 2, 3 * B).astype(np.uint8)
-        want = np.empty(B, bool)
-        for k in range(B):
-            x, y, z = ins[3 * k], ins[3 * k + 1], ins[3 * k + 2]
-            bx, by, bz = bits[3 * k], bits[3 * k + 1], bits[3 * k + 2]
-            if kinds[k] == 0: c.output(c.and_(x, y)); want[k] = bx & by
-            elif kinds[k] == 1: c.output(c.or_(x, y)); want[k] = bx | by
-            elif kinds[k] == 2: c.output(c.xor(x, y)); want[k] = bx ^ by
-            else: c.output(c.mux(x, y, z)); want[k] = by if bx else bz
+        c, bits, want = mixed_circuit(B, g)
         inputs = sk.encrypt_bool(bits, seed0=1)
         el, outs, depth, el_host, outs_host = timed_circuit(ctx, c, inputs, args, world, device)
         ok = bool(np.array_equal(sk.decrypt_bool(outs), want)) and bool(np.array_equal(outs, outs_host))
@@ -461,13 +474,19 @@ def run_workload(args, rank, world, device):
 
 def run_single_process(args):
     """All --gpus devices from this one process through tfhe_gpu_create_multi:
-    the library broadcasts the key over RCCL itself and runs one host thread per
-    device.  Host-buffer gate batches (PCIe in the timed region)."""
+    the library broadcasts the key over RCCL itself (a device listed twice gets
+    a device-to-device copy) and runs one host thread per device.  Host-buffer
+    entry points (PCIe in the timed region).  --workload nand (gate batches),
+    mixed (config 4's circuit: components over the devices, or the level split
+    with --opt circuit_split=2) or lut (config 5).  After the timed steps the
+    same inputs run once on a single-device context with the same seeded key:
+    `words_equal_one_device` says whether every output word matches."""
     n = args.gpus
     devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n))
     if len(devices) != n:
         raise SystemExit(f"bench.py: --devices lists {len(devices)} ids for --gpus {n}")
-    ctx = tfhe_amd.Context.multi(args.params, devices=devices)
+    pname = "uint4" if args.workload == "lut" else args.params
+    ctx = tfhe_amd.Context.multi(pname, devices=devices)
     apply_opts(ctx, args)
     p = ctx.params
     t0 = time.perf_counter()
@@ -475,29 +494,65 @@ def run_single_process(args):
     keygen_s = time.perf_counter() - t0
     B = args.global_batch or args.batch * n
     g = np.random.default_rng(1000)
-    a_bits = g.integers(0, 2, B).astype(np.uint8)
-    b_bits = g.integers(0, 2, B).astype(np.uint8)
-    A = sk.encrypt_bool(a_bits, seed0=1_000_000)
-    Bc = sk.encrypt_bool(b_bits, seed0=5_000_000)
-    ops = np.zeros(B, np.uint8)
+    extra = {}
+    if args.workload == "nand":
+        a_bits = g.integers(0, 2, B).astype(np.uint8)
+        b_bits = g.integers(0, 2, B).astype(np.uint8)
+        A = sk.encrypt_bool(a_bits, seed0=1_000_000)
+        Bc = sk.encrypt_bool(b_bits, seed0=5_000_000)
+        ops = np.zeros(B, np.uint8)
+        run = lambda c: c.gate_batch(ops, A, Bc)  # noqa: E731
+        check = lambda out: bool(np.array_equal(sk.decrypt_bool(out), ~(a_bits.astype(bool) & b_bits.astype(bool))))  # noqa: E731
+        metric, unit, units = METRIC + " [single-process multi-device context, host buffers]", "gate-bootstraps/s", B
+        workload = f"{B} NAND gate bootstraps per step"
+    elif args.workload == "mixed":
+        circ, bits, want = mixed_circuit(B, g)
+        inputs = sk.encrypt_bool(bits, seed0=1)
+        run = lambda c: circ.run(c, inputs)[0]  # noqa: E731
+        check = lambda out: bool(np.array_equal(sk.decrypt_bool(out), want))  # noqa: E731
+        metric, unit, units = "gates/sec (mixed AND/OR/XOR/MUX, 128-bit) [single-process multi-device context]", "gates/s", B
+        workload = f"{B} mixed AND/OR/XOR/MUX gates per step (config 4)"
+    elif args.workload == "lut":
+        m = 16
+        tv = tfhe_amd.lut_generate(p, m, lambda x: (x * x + 3) % m)
+        msgs = g.integers(0, m, B).astype(np.uint32)
+        cts = sk.encrypt_lwe_message(msgs, m, seed0=1)
+        run = lambda c: c.bootstrap_lut_batch(cts, tv)  # noqa: E731
+        check = lambda out: bool(np.array_equal(sk.decrypt_lwe_message(out, m), (msgs * msgs + 3) % m))  # noqa: E731
+        metric, unit, units = "programmable bootstraps/sec (UINT4 LUT) [single-process multi-device context]", "bootstraps/s", B
+        workload = f"{B} UINT4 LUT bootstraps per step (config 5)"
+    else:
+        raise SystemExit("bench.py --single-process: --workload nand, mixed or lut")
     for _ in range(args.warmup):
-        out = ctx.gate_batch(ops, A, Bc)
+        out = run(ctx)
+    boots0 = ctx.device_bootstraps()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = ctx.gate_batch(ops, A, Bc)
+        out = run(ctx)
     el = time.perf_counter() - t0
-    ok = bool(np.array_equal(sk.decrypt_bool(out), ~(a_bits.astype(bool) & b_bits.astype(bool))))
-    line = {"metric": METRIC + " [single-process multi-device context, host buffers]", "value": round(B * args.steps / el, 2),
-            "unit": "gate-bootstraps/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: fresh encryptions of uniform random bits under a seeded key (sk 42, ck 43)",
-            "config": {"workload": f"{B} NAND gate bootstraps per step over {n} device(s) {devices} of one context "
-                                   f"(tfhe_gpu_create_multi; keygen + key broadcast {keygen_s:.1f} s, untimed)",
-                       "global_batch": B, "params": args.params, "parallelism": f"dp{n} (one process)"},
-            "kernels": ctx.last_kernels(), "decrypt_check": ok}
-    print(json.dumps(line), flush=True)
+    per_dev = ((ctx.device_bootstraps() - boots0) // max(1, args.steps)).tolist()
+    ok = check(out)
+    if args.workload == "mixed":
+        extra["level_issue_us"] = ctx.get_option("level_issue_us")  # the level split's host issue time
+        extra["circuit_split"] = ctx.get_option("circuit_split")
+    kernels = ctx.last_kernels()
     ctx.close()
+    one = tfhe_amd.Context(pname, devices[0])  # the same seeded key on one device
+    apply_opts(one, args)
+    one.keygen(42, 43)
+    same = bool(np.array_equal(run(one), out))
+    one.close()
+    line = {"metric": metric, "value": round(units * args.steps / el, 2), "unit": unit, "n_gpus": n, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: fresh encryptions of uniform random inputs under a seeded key (sk 42, ck 43)",
+            "config": {"workload": f"{workload} over {n} device(s) {devices} of one context "
+                                   f"(tfhe_gpu_create_multi; keygen + key broadcast {keygen_s:.1f} s, untimed)",
+                       "global_batch": B, "params": pname, "parallelism": f"dp{n} (one process)"},
+            "kernels": kernels, "bootstraps_per_device_per_step": per_dev,
+            "decrypt_check": ok, "words_equal_one_device": same}
+    line.update(extra)
+    print(json.dumps(line), flush=True)
 
 
 def spawn_ranks(args) -> int:
@@ -526,6 +581,8 @@ def main():
                     help="gates per step over all GPUs, split ceil(G/N) per GPU (strong scaling)")
     ap.add_argument("--params", default="128")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--prof-steps", type=int, default=50,
+                    help="steps of the untimed profiled pass (HIP events per launch) after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--single-process", action="store_true",
@@ -601,8 +658,10 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
+    ctx.sync()
     ties0 = ctx.near_tie_items()
-    ctx.profile_begin()
+    # the timed region: K steps and nothing else (no per-launch events: they cost 0.5-0.9 ms
+    # per step at 2,048-4,096 gates, profiles/r04k_batch_sizes.txt)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -610,8 +669,15 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    br_ms, ks_ms, launches = ctx.profile_end()  # synchronises: the device error word and the guard's counter
+    ctx.sync()  # the device error word of the timed launches, and the guard's counter
     recomputed = ctx.near_tie_items() - ties0
+    # kernel averages from a separate, untimed pass of the same steps with HIP events
+    # recorded around every blind-rotation and key-switch launch on the launch stream
+    prof_steps = max(1, min(args.steps, args.prof_steps))
+    ctx.profile_begin()
+    for _ in range(prof_steps):
+        step()
+    br_ms, ks_ms, launches = ctx.profile_end()
 
     stats = torch.tensor([elapsed, 0.0 if correct else 1.0], dtype=torch.float64, device=device)
     if world > 1:
@@ -636,6 +702,10 @@ def main():
             "roofline": roof,
             "key_bytes_consumed": hbm,
             "key_switch": {"kernel": " + ".join(kernels.split(" + ")[1:]), "avg_ms": round(ks_avg_s * 1e3, 3)},
+            "kernel_timing": {"profiled_steps": prof_steps, "launches": launches,
+                              "note": "kernel averages (roofline.kernel_avg_ms, key_switch.avg_ms) come from an "
+                                      "untimed pass of profiled_steps steps after the timed region, HIP events "
+                                      "around each launch on its stream; the timed steps carry no events"},
             "margin_guard": {"recomputed_items": recomputed, "items": B * args.steps,
                              "note": "fused arithmetic; items that round a value 1/4 or more off its integer are "
                                      "redone in the reference's expression trees inside the timed launches "

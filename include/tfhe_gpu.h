@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 5  /* 5: _dev LUT / re-encryption / circuit entries; BR forms 2 and 4 removed */
+#define TFHE_GPU_ABI_VERSION 6  /* 6: tfhe_gpu_build_kind; BR forms 6/7 A/B-only, BR_LOADER / BR_SYNC = 1 only;
+                                   5: _dev LUT / re-encryption / circuit entries; BR forms 2 and 4 removed */
 
 enum {
     TFHE_OK = 0,
@@ -72,6 +73,13 @@ typedef struct {
 typedef struct tfhe_gpu_ctx tfhe_gpu_ctx;
 
 int         tfhe_gpu_abi_version(void);
+/* TFHE_BUILD_PRODUCT for the product library; TFHE_BUILD_AB for a development
+ * build (knock-out, timing or losing-form variants: tools/ab_forms.sh,
+ * tools/libvar_build.sh, a Makefile EXTRA), which every tfhe_gpu_create*
+ * refuses (TFHE_ERR_INVALID) unless the environment sets
+ * TFHE_ALLOW_AB_BUILD=1.  (ABI 6) */
+enum { TFHE_BUILD_PRODUCT = 0, TFHE_BUILD_AB = 1 };
+int         tfhe_gpu_build_kind(void);
 /* 16 hex digits of the sha256 of the kernels object this library was linked
  * from (its gfx950 code): measurements (PMC records) are tagged with it. */
 const char *tfhe_gpu_build_id(void);
@@ -143,13 +151,13 @@ int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
  * fastest forms).  Set on a context before use; a multi-device context
  * passes them to every device.  TFHE_ERR_INVALID for an unknown key or value. */
 enum {
-    TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 3 latency (2 split and
-                                     4 pair were removed in round 4: TFHE_ERR_INVALID),
-                                     5 octo (8 items per workgroup, two gate waves per SIMD), 6 duo (two
-                                     computing waves per item on one SIMD, no barriers in the step loop),
-                                     7 the latency form with split transforms at L = 3 (measured slower,
-                                     DESIGN.md §4.2) */
-    TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (default), 0 gate waves do */
+    TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 3 latency, 5 octo (8 items
+                                     per workgroup, two gate waves per SIMD; L = 1 only).  2 split and 4
+                                     pair were removed in round 4; 6 duo and 7 the split-transform latency
+                                     form (both measured slower) exist only in A/B
+                                     libraries since round 5 (tools/ab/): TFHE_ERR_INVALID here */
+    TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (the only value since
+                                     round 5; 0, the gate waves issuing them, was removed) */
     TFHE_OPT_KS_FORM = 3,         /* key switch: 3 auto (default: the one-hot GEMM on the matrix
                                      cores for basebit 2 and 5, else lanes), 0 lanes / ring,
                                      1 select / gather, 2 the GEMM at any batch (basebit 2; other
@@ -163,9 +171,9 @@ enum {
     TFHE_OPT_TWIDDLES = 8,        /* cos/sin source of the FFT tables: TFHE_TWIDDLES_* (set before a key
                                      is generated: keygen transforms the key with these tables) */
     TFHE_OPT_ARITH = 9,           /* blind-rotation f64 arithmetic: TFHE_ARITH_* */
-    TFHE_OPT_BR_SYNC = 10,        /* whole form with loader waves: 1 per-slot LDS counters (default: gate
-                                     waves wait for their data, not for each other), 0 a workgroup
-                                     barrier per BK row pair */
+    TFHE_OPT_BR_SYNC = 10,        /* whole form: 1 per-slot LDS counters (gate waves wait for their data,
+                                     not for each other; the only value since round 5: 0, a workgroup
+                                     barrier per BK row pair, was removed) */
     TFHE_OPT_BR_SPIN_CAP = 11,    /* polls before one slot-counter wait gives up and sets the device
                                      error word (0 = default, 2^22 sleep units; fault-injection tests
                                      set a few polls to see TFHE_ERR_DEVICE come back) */
@@ -335,7 +343,7 @@ int tfhe_gpu_gate_batch_dev(tfhe_gpu_ctx *ctx, const uint8_t *ops_dev, const uin
 int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *ctx, const uint32_t *in_dev, uint32_t *out_dev,
                                  size_t B);
 /* tfhe_gpu_bootstrap_lut_batch on device buffers (the test vector too: 2N
- * words of a TRLWE), single-device contexts. */
+ * words of a TRLWE), single-device contexts (TFHE_ERR_INVALID on a multi-device one). */
 int tfhe_gpu_bootstrap_lut_batch_dev(tfhe_gpu_ctx *ctx, const uint32_t *in_dev, const uint32_t *testvec_dev,
                                      uint32_t *out_dev, size_t B);
 /* tfhe_gpu_reencrypt_batch on device buffers (B TLWELv0 of n + 1 words each),

@@ -31,7 +31,46 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 5
+    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 6
+
+
+def test_library_is_not_an_ab_build():
+    """The product library carries no knock-out, timing or losing-form variant
+    (VERDICT r04 item 3): tfhe_gpu_build_kind says PRODUCT.  Any development
+    -D build (Makefile EXTRA, tools/ab_forms.sh, tools/libvar_build.sh) reports
+    TFHE_BUILD_AB, which tfhe_gpu_create refuses without TFHE_ALLOW_AB_BUILD=1;
+    the product kernel source has no such switch left (a TFHE_KO_* or A/B define
+    there would be a silent knob again)."""
+    assert tfhe_amd.build_kind() == tfhe_amd.BUILD_PRODUCT
+    src = open(os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_kernels.hip")).read()
+    src += open(os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_device.hpp")).read()
+    src += open(os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_kernels_whole.hip")).read()
+    assert "TFHE_KO_" not in src
+    # the only conditionals left: phase timing (itself an A/B build) and the build tag
+    assert set(re.findall(r"^#\s*if(?:n?def)?\s+(\w+)", src, flags=re.M)) == {"TFHE_PHASE_PROF", "TFHE_AB_BUILD"}
+    assert sum(1 for _ in open(os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_kernels.hip"))) <= 3000
+
+
+def test_ab_build_is_refused_without_the_opt_in(tmp_path):
+    """A library built with a development define (Makefile EXTRA) reports
+    TFHE_BUILD_AB and its tfhe_gpu_create fails before touching a device
+    unless TFHE_ALLOW_AB_BUILD=1 (checked in a child process: one HIP library
+    per process)."""
+    import subprocess
+    import sys
+    out = tmp_path / "lib"
+    r = subprocess.run(["make", "-s", "-j4", "-C", os.path.join(ROOT, "zig-tfhe_amd"), f"OUT={out}", "EXTRA=-DTFHE_ABI_TEST_DEFINE",
+                        f"{out}/libtfhe_gpu.so"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    code = ("import ctypes as C, sys; sys.path.insert(0, %r); import tfhe_amd; lib = tfhe_amd.load_library(); "
+            "p = tfhe_amd.make_params('128'); h = C.c_void_p(); "
+            "print(tfhe_amd.build_kind(), lib.tfhe_gpu_create(C.byref(p), 1, C.byref(h)), "
+            "lib.tfhe_gpu_last_error(None).decode())" % os.path.join(ROOT, "zig-tfhe_amd"))
+    env = dict(os.environ, TFHE_GPU_LIB=str(out / "libtfhe_gpu.so"))
+    env.pop("TFHE_ALLOW_AB_BUILD", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    kind, rc, msg = r.stdout.strip().split(" ", 2)
+    assert (int(kind), int(rc)) == (tfhe_amd.BUILD_AB, tfhe_amd.ERR_INVALID) and "A/B build" in msg
 
 
 def test_library_is_gfx950_code_object():

@@ -200,3 +200,50 @@ def test_key_blob_roundtrip_through_broadcast(oracle):
         c1.close()
     finally:
         dist.destroy_process_group()
+
+
+def _worker_subgroup(rank, world, port, corrupt, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        group = dist.new_group([1, 2])  # every rank takes part in new_group
+        if rank == 0:
+            q.put((rank, "not in group", True))
+            return
+        ctx = HostCtx(0 if rank == 1 else 1)  # global rank 1 holds the key, rank 2 has none
+        ctx.corrupt_import = corrupt and rank == 2
+        try:
+            tfhe_dist.broadcast_cloud_key(ctx, "cpu", src=1, group=group)
+            ref = HostCtx(0)
+            q.put((rank, "ok", np.array_equal(ctx.bk, ref.bk) and np.array_equal(ctx.ksk, ref.ksk)
+                   and np.array_equal(ctx.tv, ref.tv)))
+        except RuntimeError as e:
+            q.put((rank, str(e), False))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_gloo_key_broadcast_in_a_subgroup(corrupt):
+    """broadcast_cloud_key / check_key_fingerprints over a process subgroup
+    {1, 2} of a world of 3 with src = global rank 1 (group rank 0): torch's
+    broadcast takes the global rank, the all-gather list is indexed by group
+    rank.  The key arrives on rank 2; a corrupted import there is
+    named by its GLOBAL rank on both members."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_subgroup, args=(r, world, port, corrupt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r for r, _, _ in res] == [0, 1, 2]
+    for r, msg, ok in res[1:]:
+        if corrupt:
+            assert "differs" in msg and "[2]" in msg and "rank 1's" in msg, msg
+        else:
+            assert msg == "ok" and ok, (r, msg)

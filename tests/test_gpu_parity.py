@@ -112,57 +112,67 @@ def test_key_switch_gemm_full_batches(oracle, B):
 
 
 # ---- blind rotation / bootstrap ---------------------------------------------
-@pytest.mark.parametrize("form", ["whole", "whole-noloader", "whole-reference", "whole-noloader-reference",
-                                  "whole-barrier", "whole-barrier-reference", "wide",
-                                  "octo", "octo-reference", "duo", "duo-reference", "wide-reference", "wide2",
-                                  "wide2-reference"])
+@pytest.mark.parametrize("form", ["whole", "whole-reference", "wide", "wide-reference", "octo", "octo-reference"])
 @pytest.mark.parametrize("pname,B", [("80", 3), ("128", 2), ("uint4", 2)])
 def test_blind_rotate_vs_oracle(oracle, pname, B, form):
-    """All kernel forms (1 wave per item with or without loader waves, fused or
-    reference arithmetic / 2 waves per item / 8 waves per item) bit-exact."""
+    """Every product kernel form (1 wave per item with loader waves / 8 waves
+    per item / the octo form's 8 items per workgroup at L = 1), fused or
+    reference arithmetic, bit-exact.  The octo form exists at L = 1 only: the
+    option is refused at L = 3."""
     c, k = ctx_for(oracle, pname)
+    if form.startswith("octo") and pname != "uint4":
+        with pytest.raises(tfhe_amd.TfheError, match="L = 1 only"):
+            c.set_option("br_form", "octo")
+        assert c.get_option("br_form") == 0
+        return
     cts = u32rand(rng(6), B, k.p.n + 1)  # uniform TLWE: bit-exactness only
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
     # odd batch sizes leave idle item slots in the last workgroup
     cts5 = u32rand(rng(16), 5, k.p.n + 1)
     want5 = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts5])
-    with c.options(br_form=form.split("-")[0], br_loader=int("noloader" not in form),
-                   arith=int(form.endswith("reference")), br_sync=int("barrier" not in form)):
+    with c.options(br_form=form.split("-")[0], arith=int(form.endswith("reference"))):
         assert np.array_equal(c.blind_rotate_batch(cts), want)
-        if form.startswith("whole"):  # fused arithmetic only where the external product is exact (SMALL)
-            assert c.last_kernels().endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
-        if form.startswith("duo"):  # L = 1 (UINT4) runs the duo form in the reference's trees too
-            assert c.last_kernels().startswith("k_blind_rotate_duo<") == (pname == "uint4" or form == "duo")
-        prefix = {"whole": "k_blind_rotate<", "octo": "k_blind_rotate_octo<",
-                  # wide2 (split transforms) exists at L = 3; UINT4 (L = 1) runs the round-3 latency form
-                  "wide": "k_blind_rotate_wide<",
-                  "wide2": "k_blind_rotate_wide2<" if pname != "uint4" else "k_blind_rotate_wide<"}
-        if form.split("-")[0] in prefix:
-            assert c.last_kernels().startswith(prefix[form.split("-")[0]])
+        # fused arithmetic only where the external product is exact (SMALL)
+        assert c.last_kernels().split(" + ")[0].endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
+        prefix = {"whole": "k_blind_rotate<", "octo": "k_blind_rotate_octo<", "wide": "k_blind_rotate_wide<"}
+        assert c.last_kernels().startswith(prefix[form.split("-")[0]])
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
 
-@pytest.mark.parametrize("form,loader,sync", [("whole", 1, 1), ("whole", 1, 0), ("whole", 0, 0),
-                                              ("octo", 1, 0), ("duo", 1, 0)])
-def test_whole_form_every_idle_slot_count(oracle, form, loader, sync):
+@pytest.mark.parametrize("form,pname", [("whole", "80"), ("octo", "uint4")])
+def test_whole_form_every_idle_slot_count(oracle, form, pname):
     """Whole form at B = 1..8: the last workgroup has 3, 2, 1 or 0 idle gate slots
-    (clamped copies of the last item: they read in bounds, follow the barrier
-    schedule and store nothing); the octo form (8 items per workgroup) at B = 1..9
-    has 7..0 idle slots.  Regression for the round-1 development fault in
-    test_blind_rotate_vs_oracle[80-3-whole]."""
-    c, k = ctx_for(oracle, "80")
+    (clamped copies of the last item: they read in bounds, follow the slot
+    schedule and store nothing); the octo form (8 items per workgroup, L = 1) at
+    B = 1..9 has 7..0 idle slots.  Regression for the round-1 development fault
+    in test_blind_rotate_vs_oracle[80-3-whole]."""
+    c, k = ctx_for(oracle, pname)
     cts = u32rand(rng(17), 9, k.p.n + 1)
     want = np.array([oracle.blind_rotate(k.p, t, k.ck.testvec, k.ck.bk, k.ck.offset) for t in cts])
-    with c.options(br_form=form, br_loader=loader, br_sync=sync):
+    with c.options(br_form=form):
         for B in range(1, 10 if form == "octo" else 9):
             assert np.array_equal(c.blind_rotate_batch(cts[:B]), want[:B]), B
 
 
-@pytest.mark.parametrize("form", ["whole", "octo", "wide"])
-def test_bootstrap_without_key_switch(oracle, form):
+@pytest.mark.parametrize("name,value", [("br_form", 6), ("br_form", 7), ("br_form", 2), ("br_form", 4),
+                                        ("br_loader", 0), ("br_sync", 0)])
+def test_ab_only_forms_are_refused(oracle, name, value):
+    """The product library carries only its dispatchable forms: the duo and
+    split-transform latency forms (A/B libraries, tools/ab/), the removed split
+    and pair forms and the gate-wave-DMA / per-pair-barrier variants are
+    refused, and the context keeps its defaults."""
+    assert tfhe_amd.build_kind() == tfhe_amd.BUILD_PRODUCT
+    c, _ = ctx_for(oracle, "80")
+    with pytest.raises(tfhe_amd.TfheError):
+        c.set_option(name, value)
+    assert c.get_option(name) == tfhe_amd.OPTION_DEFAULTS[name]
+
+
+@pytest.mark.parametrize("form,pname", [("whole", "80"), ("wide", "80"), ("octo", "uint4")])
+def test_bootstrap_without_key_switch(oracle, form, pname):
     """VanillaBootstrap.bootstrapWithoutKeySwitch (vanilla.zig:58-69) and the
     strategy mirror: blind rotation + the hybrid sampleExtractIndex2."""
-    c, k = ctx_for(oracle, "80")
+    c, k = ctx_for(oracle, pname)
     cts = u32rand(rng(26), 3, k.p.n + 1)
     want = np.array([oracle.bootstrap_without_key_switch(k.p, t, k.ck) for t in cts])
     want1 = oracle.bootstrap(k.p, cts[1], k.ck)
@@ -233,12 +243,11 @@ def test_nand_batch_1024_128bit(oracle):
     assert np.array_equal(c.gate_batch(np.zeros(64, np.uint8), A[:64], B[:64]), out[:64])
 
 
-@pytest.mark.parametrize("loader", [1, 0])
-def test_gate_batch_rounds_and_tail(oracle, loader):
+def test_gate_batch_rounds_and_tail(oracle):
     """2,348 mixed gates (80-bit): two whole-form rounds of 1,024 plus a 300-gate tail
     that launch_blind_rotate hands to the latency form, on the plain (non-gathered)
     input path whose tail pointers it offsets.  Truth table for all, oracle bits at
-    the round and tail boundaries, with and without loader waves."""
+    the round and tail boundaries."""
     c, k = ctx_for(oracle, "80")
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
     g = rng(31)
@@ -248,8 +257,7 @@ def test_gate_batch_rounds_and_tail(oracle, loader):
     b_bits = g.integers(0, 2, n).astype(np.uint8)
     A = sk.encrypt_bool(a_bits, seed0=31_000)
     B = sk.encrypt_bool(b_bits, seed0=41_000)
-    with c.options(br_loader=loader):
-        out = c.gate_batch(ops, A, B)
+    out = c.gate_batch(ops, A, B)
     ab, bb = a_bits.astype(bool), b_bits.astype(bool)
     want_bits = np.zeros(n, bool)
     for o in range(10):  # TRUTH below works on numpy bool arrays
@@ -261,7 +269,7 @@ def test_gate_batch_rounds_and_tail(oracle, loader):
     assert np.array_equal(out[idx], want)
     # the host-buffer pipeline (TFHE_OPT_HOST_PIPELINE: 256-item chunks on 4 streams
     # through pinned staging) gives the same words
-    with c.options(br_loader=loader, host_pipeline=1):
+    with c.options(host_pipeline=1):
         assert np.array_equal(c.gate_batch(ops, A, B), out)
         assert "k_key_switch_gemm<" in c.last_kernels()  # every chunk: the same key-switch form
 
@@ -630,7 +638,7 @@ def test_options_validation_and_report(oracle):
     with pytest.raises(tfhe_amd.TfheError):
         c.set_option("br_form", 9)
     assert c.lib.tfhe_gpu_set_option(c.h, 99, 0) == -1
-    for removed in (2, 4):  # the split and pair forms, removed in round 4
+    for removed in (2, 4, 6, 7):  # split, pair (removed in round 4); duo, wide2 (A/B libraries only)
         assert c.lib.tfhe_gpu_set_option(c.h, 1, removed) == -1
     assert c.get_option("br_form") == 0
     g = rng(91)
@@ -641,19 +649,18 @@ def test_options_validation_and_report(oracle):
     with c.options(arith=tfhe_amd.ARITH_REFERENCE):
         c.bootstrap_batch(cts)
         assert c.last_kernels() == "k_blind_rotate_wide<3,true,false> (latency form) + " + gemm
-    with c.options(br_form="wide2"):  # the split-transform latency form (round 4, slower), forced
+    with c.options(br_form="whole"):
         c.bootstrap_batch(cts)
-        assert c.last_kernels() == "k_blind_rotate_wide2<3,true,true> (latency form, split transforms, fused) + " + gemm
+        assert c.last_kernels() == "k_blind_rotate<3,true,true> (whole form, fused) + " + gemm
     with c.options(ks_form=0):
         c.bootstrap_batch(cts)
         assert c.last_kernels().endswith("k_key_switch_lanes<9,2,32,4,1>")
 
 
-def test_slot_counters_and_barrier_agree_at_full_size(oracle):
-    """The whole form's two BK-slot protocols (LDS slot counters, the default, and a
-    workgroup barrier per row pair; TFHE_OPT_BR_SYNC) give identical words on a full
-    and a ragged headline-size batch (256 / 257 workgroups, every CU), and the NAND
-    truth table decrypts right."""
+def test_whole_form_full_and_ragged_headline_batches(oracle):
+    """The whole form (slot-counter protocol) on a full and a ragged headline-size
+    batch (256 / 257 workgroups, every CU): identical to the reference-tree
+    kernel, the NAND truth table decrypts right, and a sample matches the oracle."""
     c, k = ctx_for(oracle, "128")
     sk = tfhe_amd.SecretKey(c.params, k.k0, k.k1)
     g = rng(95)
@@ -661,17 +668,19 @@ def test_slot_counters_and_barrier_agree_at_full_size(oracle):
         a_bits, b_bits = g.integers(0, 2, Bn).astype(np.uint8), g.integers(0, 2, Bn).astype(np.uint8)
         A, B = sk.encrypt_bool(a_bits, seed0=95_000), sk.encrypt_bool(b_bits, seed0=96_000)
         ops = np.zeros(Bn, np.uint8)
-        with c.options(br_form="whole", br_sync=1):
-            flags = c.gate_batch(ops, A, B)
-            assert "slot counters" in c.last_kernels()
-        with c.options(br_form="whole", br_sync=0):
-            bar = c.gate_batch(ops, A, B)
-            assert "slot counters" not in c.last_kernels()
-        assert np.array_equal(flags, bar)
-        assert np.array_equal(sk.decrypt_bool(flags), ~(a_bits.astype(bool) & b_bits.astype(bool)))
+        with c.options(br_form="whole"):
+            fused = c.gate_batch(ops, A, B)
+            assert c.last_kernels().startswith("k_blind_rotate<3,true,true>")
+        with c.options(br_form="whole", arith=tfhe_amd.ARITH_REFERENCE):
+            ref = c.gate_batch(ops, A, B)
+            assert c.last_kernels().startswith("k_blind_rotate<3,true,false>")
+        assert np.array_equal(fused, ref)
+        assert np.array_equal(sk.decrypt_bool(fused), ~(a_bits.astype(bool) & b_bits.astype(bool)))
+        idx = np.array([0, Bn - 1])
+        assert np.array_equal(fused[idx], oracle.gate_batch(k.p, ops[idx], A[idx], B[idx], k.ck, threads=2))
 
 
-@pytest.mark.parametrize("form", ["auto", "whole", "wide", "octo", "duo"])
+@pytest.mark.parametrize("form", ["auto", "whole", "wide"])
 def test_margin_guard_recomputes_near_ties(oracle, form):
     """under a crafted key (conftest.crafted_near_tie_case) the
     unguarded fused arithmetic parts from the reference (the oracle's fused mode

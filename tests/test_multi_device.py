@@ -246,3 +246,78 @@ def test_key_fingerprint(oracle):
     assert e.value.status == tfhe_amd.ERR_NO_KEY
     for x in (a, b, c, empty):
         x.close()
+
+
+def test_eight_shards_on_one_gpu(oracle):
+    """the 8-way split an 8-GPU node runs, rehearsed with
+    device 0 listed eight times (8 shards, 8 streams, 8 host threads, the key
+    copied to each and fingerprint-checked).  A ragged gate batch (1,027 = 7 x
+    129 + 124, the latency form on every shard), a config-4-style circuit placed
+    by components and by the forced level split, and the UINT4 LUT batch: every
+    word equal to one device's, a sample equal to the oracle's, and the work
+    spread over all eight shards."""
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0] * 8)
+    assert multi.num_devices == 8 and multi.key_fingerprint() == single.key_fingerprint()
+    sk = tfhe_amd.SecretKey(single.params, k.k0, k.k1)
+    g = rng(81)
+    B = 1027
+    ops = g.integers(0, 10, B).astype(np.uint8)
+    A, Bc = u32rand(g, B, k.p.n + 1), u32rand(g, B, k.p.n + 1)
+    before = multi.device_bootstraps()
+    got = multi.gate_batch(ops, A, Bc)
+    ran = multi.device_bootstraps() - before
+    assert ran.tolist() == [129] * 7 + [124]
+    assert np.array_equal(got, single.gate_batch(ops, A, Bc))
+    idx = np.array([0, 128, 129, 903, B - 1])  # shard boundaries
+    assert np.array_equal(got[idx], oracle.gate_batch(k.p, ops[idx], A[idx], Bc[idx], k.ck, threads=5))
+    # config 4's shape: independent AND / OR / XOR / MUX gates over their own inputs
+    n = 1600
+    c = tfhe_amd.Circuit()
+    ins = [c.input() for _ in range(3 * n)]
+    kinds = g.integers(0, 4, n)
+    for j in range(n):
+        x, y, z = ins[3 * j: 3 * j + 3]
+        c.output([c.and_, c.or_, c.xor][kinds[j]](x, y) if kinds[j] < 3 else c.mux(x, y, z))
+    bits = g.integers(0, 2, 3 * n).astype(np.uint8)
+    inputs = sk.encrypt_bool(bits, seed0=8100)
+    want, depth1 = c.run(single, inputs)
+    for split in (1, 2):  # components, then every level split over the 8 shards
+        with multi.options(circuit_split=split):
+            before = multi.device_bootstraps()
+            got, depth = c.run(multi, inputs)
+            ran = multi.device_bootstraps() - before
+        assert depth == depth1 and np.array_equal(got, want), split
+        assert ran.sum() == sum(1 for o in c.ops if o != tfhe_amd.NOT) and ran.min() > 0, ran
+        assert ran.max() - ran.min() <= (len(c.ops) // 8) // 10 + 8, ran  # within ~10 % of an even share
+        if split == 2:
+            print(f"8-shard level split: issue {multi.get_option('level_issue_us')} us for {depth + 1} levels")
+    b3 = bits.reshape(n, 3).astype(bool)
+    truth = np.where(kinds == 0, b3[:, 0] & b3[:, 1], np.where(kinds == 1, b3[:, 0] | b3[:, 1],
+                     np.where(kinds == 2, b3[:, 0] ^ b3[:, 1], np.where(b3[:, 0], b3[:, 1], b3[:, 2]))))
+    assert np.array_equal(sk.decrypt_bool(want), truth)
+    single.close()
+    multi.close()
+    # UINT4 programmable bootstrap over 8 shards (config 5's 8-GPU leg, 300 items)
+    single, k = loaded(oracle, "uint4")
+    multi, _ = loaded(oracle, "uint4", devices=[0] * 8)
+    sk = tfhe_amd.SecretKey(single.params, k.k0, k.k1)
+    tv = tfhe_amd.lut_generate(single.params, 16, lambda x: (x * x + 3) % 16)
+    msgs = g.integers(0, 16, 300).astype(np.uint32)
+    cts = sk.encrypt_lwe_message(msgs, 16, seed0=8200)
+    got = multi.bootstrap_lut_batch(cts, tv)
+    assert np.array_equal(got, single.bootstrap_lut_batch(cts, tv))
+    assert np.array_equal(sk.decrypt_lwe_message(got, 16), (msgs * msgs + 3) % 16)
+    single.close()
+    multi.close()
+
+
+def test_lut_dev_refuses_multi_device_context(oracle):
+    """tfhe_gpu_bootstrap_lut_batch_dev takes single-device contexts, like its
+    _dev siblings: a multi-device context is refused (TFHE_ERR_INVALID) instead
+    of silently running on the first device."""
+    multi, _ = loaded(oracle, "80", devices=[0, 0])
+    with pytest.raises(tfhe_amd.TfheError) as e:
+        multi.bootstrap_lut_batch_dev(0, 0, 0, 1)
+    assert e.value.status == tfhe_amd.ERR_INVALID and "single-device" in str(e.value)
+    multi.close()

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 R=$1; LIBS=$2
 for r in $(seq 1 $R); do
   for v in $LIBS; do
-    TFHE_GPU_LIB=$PWD/tools/bin/lib_$v.so timeout -k 10 200 python bench.py --workload lut --batch 4096 --steps 5 --warmup 1 > gpurun_out/abl.json 2> gpurun_out/abl.err || { echo "$v failed"; tail -5 gpurun_out/abl.err; exit 1; }
+    TFHE_ALLOW_AB_BUILD=1 TFHE_GPU_LIB=$PWD/tools/bin/lib_$v.so timeout -k 10 200 python bench.py --workload lut --batch 4096 --steps 5 --warmup 1 > gpurun_out/abl.json 2> gpurun_out/abl.err || { echo "$v failed"; tail -5 gpurun_out/abl.err; exit 1; }
     python -c "import json,sys; d=json.loads(open('gpurun_out/abl.json').read().splitlines()[-1]); print(sys.argv[1], d['value'], d['ms_per_step'], d['kernels'], d['decrypt_check'])" "$v r$r"
   done
 done

@@ -1,8 +1,7 @@
 // Development micro-benchmark: throughput of the device FFT building blocks
 // (fft512_x2 / fft512<1>) at one wave per SIMD, registers only in/out.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Izig-tfhe_amd/csrc -o tools/bin/fft_bench tools/fft_bench.hip
-#define TFHE_SINGLE_TU
-#include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
+#include "../zig-tfhe_amd/csrc/tfhe_device.hpp"
 #include <cstdio>
 using namespace tfhe;
 

@@ -1,11 +1,11 @@
 // Development tool: per-phase s_memtime breakdown of the blind-rotation kernel
 // on a 1024-gate 128-bit batch with random operands (timing only, no parity).
-//   (-DTFHE_SPIN_STATS instead of -DTFHE_PHASE_PROF: no phase marks, only the count of
-//   slot-wait polls that found the pair unpublished, i.e. slept)
+//   (round 4's -DTFHE_SPIN_STATS poll count and the duo form's phases: profiles/r04_spin_stats.txt,
+//   DESIGN.md §4.3d; the duo form now lives in tools/ab/)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DTFHE_PHASE_PROF \
 //         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
-#define TFHE_SINGLE_TU
 #include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
+#include "../zig-tfhe_amd/csrc/tfhe_kernels_whole.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -48,28 +48,15 @@ int main(int argc, char **argv) {
 #ifdef TFHE_PHASE_PROF
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
 #endif
-#ifdef TFHE_SPIN_STATS
-        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_stats), z, 4 * sizeof(unsigned long long)));
-#endif
         CK(hipEventRecord(e0));
         LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
         const char *form = argc > 2 ? argv[2] : "whole";
-        O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : form[0] == 'd' ? 6 : 1;
-        if (argc > 3) O.br_flags = atoi(argv[3]);  // whole form: 1 slot counters, 0 barriers
+        O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
         CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         unsigned long long c[128] = {0};
-#ifdef TFHE_SPIN_STATS
-        {
-            unsigned long long sp[4];
-            CK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_spin_stats), sizeof sp));
-            printf("rep %d: %.3f ms; gate-wave slot-wait polls that slept: %.3f per wave-step (%llu waves)\n", rep, ms,
-                   sp[0] / (double)(sp[1] ? sp[1] : 1) / P.n, sp[1]);
-            continue;
-        }
-#endif
 #ifdef TFHE_PHASE_PROF
         CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
 #endif
@@ -85,25 +72,14 @@ int main(int argc, char **argv) {
             }
             continue;
         }
-        if (O.br_form == 6) {  // duo form: 2 waves per gate; phases summed over both waves
-            const char *dn[8] = {"gather+tmp", "digits+fwd fft", "refill wait", "dma issue+vmcnt", "pub wait",
-                                 "mac", "hand-off", "inverse+acc"};
-            double tot = 0;
-            for (int k = 0; k < 8; k++) tot += c[k];
-            printf("rep %d: %.3f ms; duo form, s_memtime ticks per wave-step:\n", rep, ms);
-            for (int k = 0; k < 8; k++)
-                printf("  %-16s %10.1f  %5.1f%%\n", dn[k], c[k] / (2.0 * B) / P.n, 100.0 * c[k] / tot);
-            printf("  total            %10.1f\n", tot / (2.0 * B) / P.n);
-            continue;
-        }
-        const char *nm[8] = {"tmp", "fwd-fft(pairs)", "barrier1", "mac", "barrier2", "inverse+add", "tail", "dma-issue"};
+        const char *nm[8] = {"tmp", "fwd-fft(pairs)", "slot wait", "mac", "counter add", "inverse+add", "tail", "dma-issue"};
         double tot = 0;
         for (int k = 0; k < 8; k++) tot += c[k];  // whole form: [k], loaders [8 + q]
         printf("rep %d: %.3f ms; cycles per wave-step (s_memtime ticks):\n", rep, ms);
         for (int k = 0; k < 8; k++)
             printf("  %-16s %10.1f  %5.1f%%\n", nm[k], c[k] / (double)B / P.n, 100.0 * c[k] / tot);
         printf("  total            %10.1f\n", tot / B / P.n);
-        if (O.br_flags) {  // loader waves of the slot-counter variant (one per gate wave)
+        {  // loader waves (one per gate wave)
             const char *ln[3] = {"loader: DMA landing", "loader: wait gates", "loader: issue"};
             for (int k = 0; k < 3; k++) printf("  %-22s %10.1f\n", ln[k], c[8 + k] / (double)B / P.n);
         }

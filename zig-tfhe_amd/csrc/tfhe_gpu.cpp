@@ -393,6 +393,9 @@ int key_fingerprint(tfhe_gpu_ctx *c, uint64_t &bk, uint64_t &ksk) {
 // with probability ~1e-22 (9.8 sigma), so honest keys always keep the fused path.
 constexpr double FUSED_BK_SPECTRUM_MAX = 549755813888.0;  // 2^39
 int key_admission(tfhe_gpu_ctx *c) {
+    // refused until measured: a failure below (absmax launch, copy, sync) must not
+    // leave the previous key's admission in place
+    c->opts.key_fused_ok = 0;
     auto *d = reinterpret_cast<unsigned long long *>(c->d_err + 2);
     auto *h = reinterpret_cast<volatile unsigned long long *>(c->h_err + 2);
     HIPCHK(c, hipSetDevice(c->device));
@@ -481,6 +484,7 @@ void reenc_key_gen(uint32_t n, const uint32_t *key_from, uint32_t basebit, uint3
 }
 
 int broadcast_key(tfhe_gpu_ctx *c);    // multi-device key broadcast (end of file)
+bool is_multi(const tfhe_gpu_ctx *c);  // a context over more than one device (end of file)
 void destroy_shards(tfhe_gpu_ctx *c);  // sub-contexts and RCCL communicators (end of file)
 
 // FFT constant tables (fft.zig:92-106 twists, :590-616 recurrence) from the
@@ -521,11 +525,29 @@ extern "C" {
 
 int tfhe_gpu_abi_version(void) { return TFHE_GPU_ABI_VERSION; }
 
+static const char *AB_REFUSAL =
+    "tfhe_gpu_create: this library is an A/B build (tfhe_gpu_build_kind), not the product; set "
+    "TFHE_ALLOW_AB_BUILD=1 to use it for A/B runs";
+static bool ab_build_refused() {  // knock-out / timing / losing-form builds need the opt-in
+    if (tfhe_gpu_build_kind() == TFHE_BUILD_PRODUCT) return false;
+    const char *allow = std::getenv("TFHE_ALLOW_AB_BUILD");
+    return !allow || std::strcmp(allow, "1") != 0;
+}
+
+int tfhe_gpu_build_kind(void) {
+#ifdef TFHE_AB_BUILD
+    return TFHE_BUILD_AB;
+#else
+    return kernels_ab_build() || ab_forms_linked() ? TFHE_BUILD_AB : TFHE_BUILD_PRODUCT;
+#endif
+}
+
 int tfhe_gpu_create_on_device(const tfhe_params *params, int device, tfhe_gpu_ctx **out) {
     if (!out) return TFHE_ERR_INVALID;
     *out = nullptr;
     std::string why;
     if (!params_ok(params, why)) return create_fail(TFHE_ERR_INVALID, "tfhe_gpu_create: " + why);
+    if (ab_build_refused()) return create_fail(TFHE_ERR_INVALID, AB_REFUSAL);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
         return create_fail(TFHE_ERR_HIP, "device " + std::to_string(device) + " does not exist (" +
@@ -1538,6 +1560,7 @@ int tfhe_gpu_bootstrap_batch_dev(tfhe_gpu_ctx *c, const uint32_t *in_dev, uint32
 int tfhe_gpu_bootstrap_lut_batch_dev(tfhe_gpu_ctx *c, const uint32_t *in_dev, const uint32_t *testvec_dev,
                                      uint32_t *out_dev, size_t B) {
     if (!c || !testvec_dev || (B && (!in_dev || !out_dev))) return fail(c, TFHE_ERR_INVALID, "null argument");
+    if (is_multi(c)) return fail(c, TFHE_ERR_INVALID, "device-resident calls take a single-device context");
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->has_key) return fail(c, TFHE_ERR_NO_KEY, "no cloud key loaded");
     return run_bootstrap_dev(c, nullptr, in_dev, nullptr, testvec_dev, out_dev, B, RUN_BOOTSTRAP);
@@ -1723,12 +1746,21 @@ namespace {
 bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     bool ok = false;
     switch (key) {
-    case TFHE_OPT_BR_FORM: ok = v >= 0 && v <= 7 && v != 2 && v != 4; break;  // 2 split, 4 pair: removed in round 4
+    case TFHE_OPT_BR_FORM:
+        // 2 split, 4 pair: removed in round 4; 6 duo, 7 split-transform latency
+        // form: A/B libraries only since round 5 (tools/ab/); 5 octo: L = 1 only
+        ok = v == 0 || v == 1 || v == 3 || (v == 5 && c->P.L == 1) || ((v == 6 || v == 7) && ab_forms_linked());
+        if (!ok && v == 5) why = "TFHE_OPT_BR_FORM 5 (octo form) exists at L = 1 only";
+        if (!ok && (v == 6 || v == 7)) why = "TFHE_OPT_BR_FORM " + std::to_string(v) + ": an A/B-only form, not in the product library (tools/ab/)";
+        break;
     case TFHE_OPT_KS_FORM: ok = v >= 0 && v <= 3; break;
-    case TFHE_OPT_BR_LOADER:
+    case TFHE_OPT_BR_LOADER:  // the whole form always runs loader waves with slot counters (the
+    case TFHE_OPT_BR_SYNC:    // gate-wave DMA and per-pair barrier variants were removed in round 5)
+        ok = v == 1;
+        if (!ok) why = "option " + std::to_string(key) + ": only 1 (the variant with value 0 was removed in round 5)";
+        break;
     case TFHE_OPT_KS_NARROW:
-    case TFHE_OPT_CIRCUIT_PACK:
-    case TFHE_OPT_BR_SYNC: ok = v == 0 || v == 1; break;
+    case TFHE_OPT_CIRCUIT_PACK: ok = v == 0 || v == 1; break;
     case TFHE_OPT_KS_ITEM_GROUPS: ok = v == 0 || v == 1 || v == 2 || v == 4 || v == 8; break;
     case TFHE_OPT_KS_SEL_ITEMS: ok = v == 8 || v == 16 || v == 32; break;
     case TFHE_OPT_ARITH: ok = v == TFHE_ARITH_AUTO || v == TFHE_ARITH_REFERENCE || v == TFHE_ARITH_FUSED_FORCED; break;
@@ -1748,7 +1780,7 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
         break;
     default: why = "unknown option key " + std::to_string(key); return false;
     }
-    if (!ok) why = "bad value " + std::to_string(v) + " for option " + std::to_string(key);
+    if (!ok && why.empty()) why = "bad value " + std::to_string(v) + " for option " + std::to_string(key);
     return ok;
 }
 
@@ -1757,14 +1789,14 @@ int apply_option(tfhe_gpu_ctx *c, int key, int64_t v) {
     LaunchOpts &o = c->opts;
     switch (key) {
     case TFHE_OPT_BR_FORM: o.br_form = (int)v; break;
-    case TFHE_OPT_BR_LOADER: o.br_loader = (int)v; break;
+    case TFHE_OPT_BR_LOADER: break;
     case TFHE_OPT_KS_FORM: o.ks_form = (int)v; break;
     case TFHE_OPT_KS_NARROW: o.ks_narrow = (int)v; break;
     case TFHE_OPT_KS_ITEM_GROUPS: o.ks_groups = (int)v; break;
     case TFHE_OPT_KS_SEL_ITEMS: o.ks_sel_items = (int)v; break;
     case TFHE_OPT_CIRCUIT_PACK: c->circuit_pack = v; break;
     case TFHE_OPT_TWIDDLES: return v == c->twiddle_source ? TFHE_OK : build_tables(c, (int)v);
-    case TFHE_OPT_BR_SYNC: o.br_flags = (int)v; break;
+    case TFHE_OPT_BR_SYNC: break;
     case TFHE_OPT_ARITH: o.arith_strict = v == TFHE_ARITH_REFERENCE ? 1 : v == TFHE_ARITH_FUSED_FORCED ? 2 : 0; break;
     case TFHE_OPT_BR_SPIN_CAP: c->K.spin_cap = (uint32_t)v; break;
     case TFHE_OPT_HOST_PIPELINE: c->pipeline = v; break;
@@ -1795,7 +1827,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     const LaunchOpts &o = c->opts;
     switch (key) {
     case TFHE_OPT_BR_FORM: *v = o.br_form; break;
-    case TFHE_OPT_BR_LOADER: *v = o.br_loader; break;
+    case TFHE_OPT_BR_LOADER: *v = 1; break;
     case TFHE_OPT_KS_FORM: *v = o.ks_form; break;
     case TFHE_OPT_KS_NARROW: *v = o.ks_narrow; break;
     case TFHE_OPT_KS_ITEM_GROUPS: *v = o.ks_groups; break;
@@ -1805,7 +1837,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_ARITH: *v = o.arith_strict == 1 ? TFHE_ARITH_REFERENCE : o.arith_strict == 2 ? TFHE_ARITH_FUSED_FORCED : TFHE_ARITH_AUTO; break;
     case TFHE_OPT_FUSED_ADMITTED: *v = o.key_fused_ok; break;
     case TFHE_OPT_LEVEL_ISSUE_US: *v = c->level_issue_us; break;
-    case TFHE_OPT_BR_SYNC: *v = o.br_flags; break;
+    case TFHE_OPT_BR_SYNC: *v = 1; break;
     case TFHE_OPT_BR_SPIN_CAP: *v = c->K.spin_cap; break;
     case TFHE_OPT_HOST_PIPELINE: *v = c->pipeline; break;
     case TFHE_OPT_CIRCUIT_SPLIT: *v = c->circuit_split; break;
@@ -1896,7 +1928,10 @@ void destroy_shards(tfhe_gpu_ctx *c) {
 // device appears twice.  The test vector / offset are host state (8 KB).
 int broadcast_key(tfhe_gpu_ctx *c) {
     int rc0 = key_admission(c);  // every key load ends here: admit the fused arithmetic or not
-    if (rc0) return rc0;
+    if (rc0) {  // an unmeasured key is not a loaded key
+        c->has_key = false;
+        return rc0;
+    }
     if (c->shards.empty()) return TFHE_OK;
     const size_t D = c->shards.size();
     for (size_t d = 1; d < D; d++) {
@@ -2257,6 +2292,7 @@ int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int 
     for (int d = 0; d < num_devices; d++) devs[d] = devices ? devices[d] : d;
     std::string why;
     if (!params_ok(params, why)) return create_fail(TFHE_ERR_INVALID, "tfhe_gpu_create_multi: " + why);
+    if (ab_build_refused()) return create_fail(TFHE_ERR_INVALID, AB_REFUSAL);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess) return create_fail(TFHE_ERR_HIP, "hipGetDeviceCount failed");
     for (int d : devs)
@@ -2319,6 +2355,7 @@ int tfhe_gpu_create(const tfhe_params *params, int num_devices, tfhe_gpu_ctx **o
     std::string why;
     if (num_devices < 1 || !params_ok(params, why))
         return create_fail(TFHE_ERR_INVALID, num_devices < 1 ? "num_devices < 1" : "tfhe_gpu_create: " + why);
+    if (ab_build_refused()) return create_fail(TFHE_ERR_INVALID, AB_REFUSAL);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || num_devices > ndev)
         return create_fail(TFHE_ERR_HIP, std::to_string(num_devices) + " device(s) requested, " +

@@ -77,9 +77,7 @@ struct DevTables {
 // for A/B runs and parity tests.  `used` (may be NULL) receives the name of
 // the kernel a launcher ran.
 struct LaunchOpts {
-    int br_form = 0;     // 0 auto, 1 whole, 2 split, 3 latency (wide), 4 pair
-    int br_loader = 1;   // whole form: 1 loader waves issue the BK DMAs, 0 the gate waves do
-    int br_flags = 1;    // whole form with loader waves: 1 slot counters (default), 0 a barrier per row pair
+    int br_form = 0;     // 0 auto, 1 whole, 3 latency (wide), 5 octo (L = 1); 6 duo, 7 wide2 (A/B libraries only)
     int ks_form = 3;     // 0 lanes, 1 select / gather, 2 one-hot GEMM on the matrix cores (basebit 2), 3 auto
     int ks_narrow = 0;   // basebit 2: 1 forces the 32-word x 4-wave blocks
     int ks_groups = 0;   // basebit >= 5: item groups per block (0 auto = 4; 1, 2, 4, 8)
@@ -94,6 +92,18 @@ struct LaunchOpts {
 inline bool fused_allowed(const LaunchOpts &O) {
     return O.arith_strict == 2 || (O.arith_strict == 0 && O.key_fused_ok != 0);
 }
+
+// An A/B build (any -D define that changes the kernels or their timing:
+// tools/ab_forms.sh, tools/libvar_build.sh, tools/phase_prof.hip, a Makefile
+// EXTRA) compiles every unit with TFHE_AB_BUILD; tfhe_gpu_create refuses such a
+// library unless TFHE_ALLOW_AB_BUILD=1 is set (tfhe_gpu_build_kind).
+#if defined(TFHE_PHASE_PROF) && !defined(TFHE_AB_BUILD)
+#define TFHE_AB_BUILD 1
+#endif
+bool kernels_ab_build();  // tfhe_kernels.hip: this unit was compiled as an A/B build
+// The A/B-only blind-rotation forms (TFHE_OPT_BR_FORM 6, 7) are linked in
+// (tools/ab/tfhe_ab_forms.hip), i.e. this is an A/B library.
+bool ab_forms_linked();
 
 // ---- launchers (tfhe_kernels.hip); all asynchronous on `s` --------------
 // idx: NULL, or B pairs (a, b) of ciphertext indices into in_a / in_b (circuit gather)

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "029107cca9f90f89"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "fbb4a7979347ae33"; }

@@ -31,7 +31,9 @@ OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 3, "ks_narrow": 0, "
                    "host_pipeline": 0, "circuit_split": 0}
 # status codes (include/tfhe_gpu.h TFHE_ERR_*)
 ERR_INVALID, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_IO, ERR_DEVICE = -1, -2, -3, -4, -5, -6
-BR_FORMS = {"auto": 0, "whole": 1, "wide": 3, "octo": 5, "duo": 6, "wide2": 7}  # 2 split, 4 pair: removed (round 4)
+# 2 split, 4 pair: removed (round 4); 6 duo, 7 wide2: A/B libraries only (tools/ab/, round 5); 5 octo: L = 1
+BR_FORMS = {"auto": 0, "whole": 1, "wide": 3, "octo": 5, "duo": 6, "wide2": 7}
+BUILD_PRODUCT, BUILD_AB = 0, 1  # tfhe_gpu_build_kind
 TWIDDLES_GLIBC, TWIDDLES_FDLIBM = 0, 1
 ARITH_AUTO, ARITH_REFERENCE, ARITH_FUSED_FORCED = 0, 1, 2
 
@@ -83,6 +85,7 @@ u32p, f64p, u8p, vp = C.POINTER(C.c_uint32), C.POINTER(C.c_double), C.POINTER(C.
 _SIGS = {
     "tfhe_gpu_abi_version": (C.c_int, []),
     "tfhe_gpu_build_id": (C.c_char_p, []),
+    "tfhe_gpu_build_kind": (C.c_int, []),
     "tfhe_gpu_create": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(vp)]),
     "tfhe_gpu_create_on_device": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(vp)]),
     "tfhe_gpu_destroy": (None, [vp]),
@@ -192,6 +195,13 @@ def _f64(a):
 def build_id() -> str:
     """tfhe_gpu_build_id: hash of the gfx950 kernels object the loaded library carries."""
     return load_library().tfhe_gpu_build_id().decode()
+
+
+def build_kind() -> int:
+    """tfhe_gpu_build_kind: BUILD_PRODUCT, or BUILD_AB for a development build
+    (knock-out / timing / losing-form variants), which contexts refuse unless
+    TFHE_ALLOW_AB_BUILD=1."""
+    return load_library().tfhe_gpu_build_kind()
 
 
 class TfheError(RuntimeError):

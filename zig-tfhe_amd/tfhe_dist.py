@@ -25,8 +25,16 @@ def _sync(device):
         torch.cuda.synchronize(device)
 
 
+def _group_rank(group, global_rank: int) -> int:
+    """Rank within `group` of a global rank (torch.distributed's collectives
+    take `src` as a global rank; get_rank(group) and all_gather lists are
+    indexed by group rank)."""
+    import torch.distributed as dist
+    return global_rank if group is None else dist.get_group_rank(group, global_rank)
+
+
 def broadcast_cloud_key(ctx, device, src: int = 0, group=None):
-    """Rank `src` exports its device-resident key blob (BK in the device
+    """Rank `src` (a global rank, a member of `group`) exports its device-resident key blob (BK in the device
     layout, KSK, decomposition offset, test vector); every rank receives it by
     torch.distributed.broadcast — RCCL over xGMI for the nccl backend, one
     bucket per tensor — and imports it.  Nothing else crosses devices: this
@@ -39,19 +47,19 @@ def broadcast_cloud_key(ctx, device, src: int = 0, group=None):
     import torch
     import torch.distributed as dist
 
-    rank = dist.get_rank(group)
+    is_src = dist.get_rank(group) == _group_rank(group, src)
     bk_bytes, ksk_bytes = ctx.key_blob_bytes()
     bk = torch.empty(bk_bytes, dtype=torch.uint8, device=device)
     ksk = torch.empty(ksk_bytes, dtype=torch.uint8, device=device)
     meta = torch.zeros(1 + 2 * ctx.params.N, dtype=torch.int64, device=device)
-    if rank == src:
+    if is_src:
         offset, tv = ctx.export_key_device(bk.data_ptr(), ksk.data_ptr())
         _sync(device)
         meta[0] = offset
         meta[1:] = torch.from_numpy(np.asarray(tv).astype(np.int64))
     for t in (bk, ksk, meta):
         dist.broadcast(t, src, group=group)
-    if rank != src:
+    if not is_src:
         _sync(device)
         m = meta.cpu().numpy()
         ctx.import_key_device(bk.data_ptr(), ksk.data_ptr(), int(m[0]), m[1:].astype(np.uint32))
@@ -61,7 +69,7 @@ def broadcast_cloud_key(ctx, device, src: int = 0, group=None):
 
 
 def check_key_fingerprints(ctx, device, src: int = 0, group=None):
-    """Every rank's resident key must fingerprint like rank `src`'s
+    """Every rank's resident key must fingerprint like (global) rank `src`'s
     (tfhe_gpu_key_fingerprint, the same check the in-library multi-device
     broadcast makes): all-gather the (bk, ksk) sums and raise on any rank whose
     copy differs, naming it, on EVERY rank (no rank runs gates on a key that
@@ -74,9 +82,10 @@ def check_key_fingerprints(ctx, device, src: int = 0, group=None):
     mine = torch.tensor([bk_fp - (1 << 63), ksk_fp - (1 << 63)], dtype=torch.int64, device=fdev)  # u64 -> i64
     parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
     dist.all_gather(parts, mine, group=group)
-    want = parts[src].cpu()
+    want = parts[_group_rank(group, src)].cpu()
     bad = [r for r, t in enumerate(parts) if not torch.equal(t.cpu(), want)]
-    if bad:
+    if bad:  # name the global ranks
+        bad = bad if group is None else [dist.get_global_rank(group, r) for r in bad]
         raise RuntimeError(f"cloud-key broadcast: the key on rank(s) {bad} differs from rank {src}'s "
                            f"(fingerprints {[tuple(int(x) + (1 << 63) for x in t.cpu()) for t in parts]})")
 
