@@ -318,6 +318,6 @@ def test_lut_dev_refuses_multi_device_context(oracle):
     of silently running on the first device."""
     multi, _ = loaded(oracle, "80", devices=[0, 0])
     with pytest.raises(tfhe_amd.TfheError) as e:
-        multi.bootstrap_lut_batch_dev(0, 0, 0, 1)
+        multi.bootstrap_lut_batch_dev(64, 64, 64, 1)  # never dereferenced: refused first
     assert e.value.status == tfhe_amd.ERR_INVALID and "single-device" in str(e.value)
     multi.close()
