@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 6  /* 6: tfhe_gpu_build_kind; BR forms 6/7 A/B-only, BR_LOADER / BR_SYNC = 1 only;
+#define TFHE_GPU_ABI_VERSION 6  /* 6: tfhe_gpu_build_kind, tfhe_lut_generate_scaled / _full; BR forms 6/7
+                                   A/B-only, BR_LOADER / BR_SYNC = 1 only;
                                    5: _dev LUT / re-encryption / circuit entries; BR forms 2 and 4 removed */
 
 enum {
@@ -408,9 +409,16 @@ int tfhe_reenc_key_gen_asymmetric(const tfhe_params *params, const uint32_t *key
                                   size_t pk_size, double alpha, uint32_t basebit, uint32_t t, uint64_t seed0,
                                   uint32_t *out);
 /* Generator.generateLookupTableAssign (lut/generator.zig:85-135): testvec
- * (2N words, a = 0) for f given as a table f_table[x], x < m. */
+ * (2N words, a = 0) for f given as a table f_table[x], x < m, encoded by
+ * Encoder.new(m) (scale 1/(2m), encoder.zig:29-42).  Any m >= 1. */
 int tfhe_lut_generate(const tfhe_params *params, uint32_t m, const uint32_t *f_table,
                       uint32_t *testvec);
+/* The same with Encoder.withScale(m, scale) (Generator.withScale, generateLookupTableCustom;
+ * generator.zig:47-56, :202-213).  (ABI 6) */
+int tfhe_lut_generate_scaled(const tfhe_params *params, uint32_t m, double scale, const uint32_t *f_table,
+                             uint32_t *testvec);
+/* generateLookupTableFull (generator.zig:144-191): values[x] is message x's Torus value as is.  (ABI 6) */
+int tfhe_lut_generate_full(const tfhe_params *params, uint32_t m, const uint32_t *values, uint32_t *testvec);
 
 #ifdef __cplusplus
 }

@@ -333,6 +333,29 @@ class Oracle:
         self.lib.oracle_lut_generate(C.c_uint32(N), C.c_uint32(m), _ptr(f, u32p), _ptr(tv, u32p))
         return tv
 
+    def lut_generate_scaled(self, N, m, scale, f_table):
+        f = np.ascontiguousarray(f_table, dtype=np.uint32)
+        tv = np.zeros(2 * N, dtype=np.uint32)
+        self.lib.oracle_lut_generate_scaled(C.c_uint32(N), C.c_uint32(m), C.c_double(scale), _ptr(f, u32p),
+                                            _ptr(tv, u32p))
+        return tv
+
+    def lut_generate_full(self, N, m, values):
+        v = np.ascontiguousarray(values, dtype=np.uint32)
+        tv = np.zeros(2 * N, dtype=np.uint32)
+        self.lib.oracle_lut_generate_full(C.c_uint32(N), C.c_uint32(m), _ptr(v, u32p), _ptr(tv, u32p))
+        return tv
+
+    def div_round(self, a, b):
+        """divRound (lut/generator.zig:253-255)."""
+        self.lib.oracle_div_round.restype = C.c_size_t
+        return int(self.lib.oracle_div_round(C.c_size_t(a), C.c_size_t(b)))
+
+    def lut_mod_switch(self, x, size):
+        """Generator.modSwitch (lut/generator.zig:223-227)."""
+        self.lib.oracle_lut_mod_switch.restype = C.c_size_t
+        return int(self.lib.oracle_lut_mod_switch(C.c_uint32(x), C.c_size_t(size)))
+
     def encrypt_lwe_message(self, n, msg, m, alpha, key, seed):
         out = np.zeros(n + 1, dtype=np.uint32)
         self.lib.oracle_tlwe_encrypt_lwe_message(n, msg, m, alpha, _ptr(key, u32p), seed, _ptr(out, u32p))

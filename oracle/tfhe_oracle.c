@@ -933,22 +933,41 @@ void oracle_cloud_key_new(const oracle_params *p, uint64_t seed, const uint32_t 
 /* ======================================================================== */
 /* Programmable bootstrap (LUT) — lut/generator.zig:85-135, encoder.zig     */
 /* ======================================================================== */
-static size_t div_round(size_t a, size_t b) { return (a + b / 2) / b; }  /* generator.zig:253-255 */
+size_t oracle_div_round(size_t a, size_t b) { return (a + b / 2) / b; }  /* divRound, generator.zig:253-255 */
 
-void oracle_lut_generate(uint32_t N, uint32_t m, const uint32_t *f_table, uint32_t *tv) {
+/* generateLookupTableFullAssign (generator.zig:155-191): raw[divRound(xN, m) ..
+ * divRound((x+1)N, m)) = values[x]; rotate by divRound(N, 2m); negate the tail */
+void oracle_lut_generate_full(uint32_t N, uint32_t m, const uint32_t *values, uint32_t *tv) {
     uint32_t *raw = (uint32_t *)calloc(N, sizeof(uint32_t));
-    double scale = 1.0 / (2.0 * (double)m);                       /* Encoder.new encoder.zig:29-43 */
     for (uint32_t x = 0; x < m; x++) {
-        size_t start = div_round((size_t)x * N, m), end = div_round((size_t)(x + 1) * N, m);
-        uint32_t y = f_table[x];
-        uint32_t enc = oracle_f64_to_torus((double)(y % m) * scale);  /* encode :62-69 */
-        for (size_t xx = start; xx < end; xx++) raw[xx] = enc;
+        size_t start = oracle_div_round((size_t)x * N, m), end = oracle_div_round((size_t)(x + 1) * N, m);
+        for (size_t xx = start; xx < end; xx++) raw[xx] = values[x];
     }
-    size_t offset = div_round(N, 2 * (size_t)m);
+    size_t offset = oracle_div_round(N, 2 * (size_t)m);
     for (size_t i = 0; i < N; i++) tv[N + i] = raw[(i + offset) % N];
     for (size_t i = N - offset; i < N; i++) tv[N + i] = ~tv[N + i] + 1u;
     for (size_t i = 0; i < N; i++) tv[i] = 0;
     free(raw);
+}
+
+/* generateLookupTableAssign (generator.zig:85-135) with Encoder.withScale(m,
+ * scale) (encoder.zig:49-74): values[x] = f64ToTorus((f(x) mod m) * scale) */
+void oracle_lut_generate_scaled(uint32_t N, uint32_t m, double scale, const uint32_t *f_table, uint32_t *tv) {
+    uint32_t *enc = (uint32_t *)calloc(m, sizeof(uint32_t));
+    for (uint32_t x = 0; x < m; x++) enc[x] = oracle_f64_to_torus((double)(f_table[x] % m) * scale);
+    oracle_lut_generate_full(N, m, enc, tv);
+    free(enc);
+}
+
+/* Generator.new(m) (generator.zig:29-41): Encoder.new(m), scale 1/(2m) (encoder.zig:29-42) */
+void oracle_lut_generate(uint32_t N, uint32_t m, const uint32_t *f_table, uint32_t *tv) {
+    oracle_lut_generate_scaled(N, m, 1.0 / (2.0 * (double)m), f_table, tv);
+}
+
+/* Generator.modSwitch (generator.zig:223-227): (x / maxInt(u32)) * size, + 0.5, truncated, mod size */
+size_t oracle_lut_mod_switch(uint32_t x, size_t size) {
+    double scaled = ((double)x / (double)4294967295u) * (double)size;
+    return (size_t)(scaled + 0.5) % size;
 }
 
 /* encryptLweMessage / decryptLweMessage — tlwe.zig:74-117 */

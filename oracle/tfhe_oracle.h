@@ -116,6 +116,10 @@ void oracle_trgsw_encrypt_torus_fft(const oracle_params *p, uint32_t mu, double 
 /* ---- programmable bootstrap (lut generator/encoder, trgsw.zig:336-400) */
 void oracle_lut_generate(uint32_t N, uint32_t message_modulus, const uint32_t *f_table /*m*/,
                          uint32_t *testvec /*2N*/);
+void oracle_lut_generate_scaled(uint32_t N, uint32_t m, double scale, const uint32_t *f_table, uint32_t *tv);
+void oracle_lut_generate_full(uint32_t N, uint32_t m, const uint32_t *values, uint32_t *tv);
+size_t oracle_div_round(size_t a, size_t b);
+size_t oracle_lut_mod_switch(uint32_t x, size_t size);
 void oracle_tlwe_encrypt_lwe_message(uint32_t n, uint32_t msg, uint32_t m, double alpha,
                                      const uint32_t *key, uint64_t seed, uint32_t *out);
 uint32_t oracle_tlwe_decrypt_lwe_message(uint32_t n, const uint32_t *ct, uint32_t m, const uint32_t *key);

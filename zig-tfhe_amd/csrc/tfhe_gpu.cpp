@@ -1715,21 +1715,41 @@ int tfhe_decrypt_lwe_message_batch(const tfhe_params *p, const uint32_t *key, co
     return TFHE_OK;
 }
 
-int tfhe_lut_generate(const tfhe_params *p, uint32_t m, const uint32_t *f_table, uint32_t *tv) {
-    if (!p || !f_table || !tv || m == 0 || m > p->N) return TFHE_ERR_INVALID;
-    const size_t N = p->N;
+// generateLookupTableFullAssign (lut/generator.zig:155-191): message x's range
+// [divRound(xN, m), divRound((x+1)N, m)) of the raw table holds values[x]; the
+// table is rotated by divRound(N, 2m), its last divRound(N, 2m) entries negated,
+// and stored as the b polynomial (a = 0).  divRound(a, b) = (a + b/2) / b
+// (generator.zig:253-255).  Any m >= 1, as the reference (m > N leaves ranges empty).
+static void lut_from_values(size_t N, size_t m, const uint32_t *values, uint32_t *tv) {
     std::vector<uint32_t> raw(N, 0u);
-    const double scale = 1.0 / (2.0 * (double)m);
     auto div_round = [](size_t a, size_t b) { return (a + b / 2) / b; };
-    for (uint32_t x = 0; x < m; x++) {
-        size_t s = div_round((size_t)x * N, m), e = div_round((size_t)(x + 1) * N, m);
-        uint32_t enc = host::f64_to_torus((double)(f_table[x] % m) * scale);
-        for (size_t i = s; i < e; i++) raw[i] = enc;
+    for (size_t x = 0; x < m; x++) {
+        const size_t s = div_round(x * N, m), e = div_round((x + 1) * N, m);
+        for (size_t i = s; i < e; i++) raw[i] = values[x];
     }
-    size_t off = div_round(N, 2 * (size_t)m);
+    const size_t off = div_round(N, 2 * m);
     for (size_t i = 0; i < N; i++) tv[N + i] = raw[(i + off) % N];
     for (size_t i = N - off; i < N; i++) tv[N + i] = ~tv[N + i] + 1u;
     for (size_t i = 0; i < N; i++) tv[i] = 0;
+}
+
+int tfhe_lut_generate_scaled(const tfhe_params *p, uint32_t m, double scale, const uint32_t *f_table, uint32_t *tv) {
+    if (!p || !f_table || !tv || m == 0) return TFHE_ERR_INVALID;
+    std::vector<uint32_t> enc(m);
+    for (uint32_t x = 0; x < m; x++)  // Encoder.encode (encoder.zig:66-74): (f(x) mod m) * scale -> torus
+        enc[x] = host::f64_to_torus((double)(f_table[x] % m) * scale);
+    lut_from_values(p->N, m, enc.data(), tv);
+    return TFHE_OK;
+}
+
+int tfhe_lut_generate(const tfhe_params *p, uint32_t m, const uint32_t *f_table, uint32_t *tv) {
+    if (!p || m == 0) return TFHE_ERR_INVALID;
+    return tfhe_lut_generate_scaled(p, m, 1.0 / (2.0 * (double)m), f_table, tv);  // Encoder.new (encoder.zig:29-42)
+}
+
+int tfhe_lut_generate_full(const tfhe_params *p, uint32_t m, const uint32_t *values, uint32_t *tv) {
+    if (!p || !values || !tv || m == 0) return TFHE_ERR_INVALID;
+    lut_from_values(p->N, m, values, tv);
     return TFHE_OK;
 }
 

@@ -141,6 +141,8 @@ _SIGS = {
     "tfhe_decrypt_lwe_message_batch": (C.c_int, [C.POINTER(TfheParams), u32p, u32p, C.c_uint32, u32p,
                                                  C.c_size_t]),
     "tfhe_lut_generate": (C.c_int, [C.POINTER(TfheParams), C.c_uint32, u32p, u32p]),
+    "tfhe_lut_generate_scaled": (C.c_int, [C.POINTER(TfheParams), C.c_uint32, C.c_double, u32p, u32p]),
+    "tfhe_lut_generate_full": (C.c_int, [C.POINTER(TfheParams), C.c_uint32, u32p, u32p]),
     "tfhe_secret_key_new": (C.c_int, [C.POINTER(TfheParams), C.c_uint64, u32p, u32p]),
     "tfhe_gpu_reenc_key_load": (C.c_int, [vp, u32p, C.c_size_t, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
     "tfhe_gpu_reenc_key_destroy": (None, [vp]),
@@ -719,6 +721,120 @@ def lut_generate(params: TfheParams, m: int, f) -> np.ndarray:
     if rc:
         raise TfheError(f"lut_generate: {rc}")
     return tv
+
+
+class Encoder:
+    """lut/encoder.zig Encoder: message x -> f64ToTorus((x mod m) * scale);
+    new(m) uses scale 1/(2m) (encoder.zig:29-42), with_scale a custom one (:49-54)."""
+
+    def __init__(self, message_modulus: int, scale: float | None = None):
+        self.message_modulus = int(message_modulus)
+        self.scale = 1.0 / (2.0 * float(message_modulus)) if scale is None else float(scale)
+
+    @classmethod
+    def new(cls, message_modulus: int) -> "Encoder":
+        return cls(message_modulus)
+
+    @classmethod
+    def with_scale(cls, message_modulus: int, scale: float) -> "Encoder":
+        return cls(message_modulus, scale)
+
+
+class LookupTable:
+    """lut/lookup_table.zig LookupTable: a TRLWELv1 (a ++ b, 2N words) that the
+    blind rotation uses as its test vector (tfhe_gpu_bootstrap_lut_batch)."""
+
+    def __init__(self, poly=None, N: int = 1024):
+        self.poly = np.zeros(2 * N, np.uint32) if poly is None else np.array(poly, np.uint32).reshape(-1)
+
+    @classmethod
+    def new(cls, N: int = 1024) -> "LookupTable":  # :23-27
+        return cls(N=N)
+
+    @classmethod
+    def from_poly(cls, poly) -> "LookupTable":  # :33-35 (a copy of the TRLWELv1's words)
+        return cls(poly)
+
+    @property
+    def a(self):
+        return self.poly[: self.poly.size // 2]
+
+    @property
+    def b(self):
+        return self.poly[self.poly.size // 2:]
+
+    def get_poly(self) -> np.ndarray:  # :38-45
+        return self.poly
+
+    def copy_from(self, other: "LookupTable"):  # :51-54
+        self.poly[:] = other.poly
+
+    def clear(self):  # :57-61
+        self.poly[:] = 0
+
+    def is_empty(self) -> bool:  # :64-77
+        return not self.poly.any()
+
+
+class Generator:
+    """lut/generator.zig Generator over the C ABI's table generation
+    (tfhe_lut_generate_scaled / _full): poly_degree = lookup_table_size = N
+    (the reference's poly_extend_factor 1)."""
+
+    def __init__(self, encoder: Encoder, params: TfheParams | None = None):
+        self.encoder = encoder
+        self.params = params if params is not None else make_params("128")
+        self.poly_degree_ = self.lookup_table_size_ = int(self.params.N)
+
+    @classmethod
+    def new(cls, message_modulus: int, params: TfheParams | None = None) -> "Generator":  # :29-41
+        return cls(Encoder.new(message_modulus), params)
+
+    @classmethod
+    def with_scale(cls, message_modulus: int, scale: float, params: TfheParams | None = None) -> "Generator":  # :47-56
+        return cls(Encoder.with_scale(message_modulus, scale), params)
+
+    def message_modulus(self) -> int:  # :230-232
+        return self.encoder.message_modulus
+
+    def poly_degree(self) -> int:  # :235-237
+        return self.poly_degree_
+
+    def lookup_table_size(self) -> int:  # :240-242
+        return self.lookup_table_size_
+
+    def generate_lookup_table_assign(self, f, lut: LookupTable):  # :85-135
+        m = self.encoder.message_modulus
+        table = np.array([f(x) for x in range(m)], dtype=np.uint32)
+        rc = load_library().tfhe_lut_generate_scaled(C.byref(self.params), m, self.encoder.scale,
+                                                     table.ctypes.data_as(u32p), lut.poly.ctypes.data_as(u32p))
+        if rc:
+            raise TfheError(f"lut_generate_scaled: {rc}", rc)
+
+    def generate_lookup_table(self, f) -> LookupTable:  # :65-69
+        lut = LookupTable.new(self.params.N)
+        self.generate_lookup_table_assign(f, lut)
+        return lut
+
+    def generate_lookup_table_full_assign(self, f, lut: LookupTable):  # :155-191: f(x) is a Torus value
+        m = self.encoder.message_modulus
+        vals = np.array([int(f(x)) & 0xFFFFFFFF for x in range(m)], dtype=np.uint32)
+        rc = load_library().tfhe_lut_generate_full(C.byref(self.params), m, vals.ctypes.data_as(u32p),
+                                                   lut.poly.ctypes.data_as(u32p))
+        if rc:
+            raise TfheError(f"lut_generate_full: {rc}", rc)
+
+    def generate_lookup_table_full(self, f) -> LookupTable:  # :144-148
+        lut = LookupTable.new(self.params.N)
+        self.generate_lookup_table_full_assign(f, lut)
+        return lut
+
+    def generate_lookup_table_custom(self, f, message_modulus: int, scale: float) -> LookupTable:  # :202-213
+        return Generator(Encoder.with_scale(message_modulus, scale), self.params).generate_lookup_table(f)
+
+    def mod_switch(self, x: int) -> int:  # :223-227, the reference's f64 expression
+        scaled = (float(int(x) & 0xFFFFFFFF) / 4294967295.0) * float(self.lookup_table_size_)
+        return int(scaled + 0.5) % self.lookup_table_size_
 
 
 def cloud_key_write(path: str, params: TfheParams, offset: int, testvec, bk, ksk):
