@@ -188,11 +188,15 @@ enum {
                                      outputs all-gathered by peer copies before the next level) */
     TFHE_OPT_FUSED_ADMITTED = 14, /* read-only (get_option): 1 if the resident cloud key passed the fused
                                      arithmetic's admission check at load (largest BK spectrum component
-                                     <= 2^39), 0 if it was refused and TFHE_ARITH_AUTO
-                                     runs the reference's expression trees for it */
-    TFHE_OPT_LEVEL_ISSUE_US = 15  /* read-only: host microseconds the last level-split circuit_eval spent
+                                     <= 2^39 and every TRGSW row's RMS <= 0.65 x 2^31), 0
+                                     if it was refused and TFHE_ARITH_AUTO runs the reference's expression
+                                     trees for it */
+    TFHE_OPT_LEVEL_ISSUE_US = 15, /* read-only: host microseconds the last level-split circuit_eval spent
                                      issuing its per-level launches, peer copies and event waits (one
                                      host thread for all devices) */
+    TFHE_OPT_KEY_ROW_RMS_PPM = 16 /* read-only: the resident key's largest TRGSW row RMS / 2^31, in
+                                     millionths (the admission's row-energy rule admits <= 650000;
+                                     keygen'd keys ~600000; ABI 6) */
 };
 /* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
  * runs fused multiply-adds in the reference's operation order, with a margin

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -128,6 +129,7 @@ struct tfhe_gpu_ctx {
     int64_t twiddle_source = TFHE_TWIDDLES_GLIBC;
     bool key_from_keygen = false;  // the resident BK was transformed with this context's tables
     double bk_absmax = 0.0;        // largest |BK spectrum component| of the resident key, reference scale
+    double bk_row_rms = 0.0;       // largest TRGSW row RMS / 2^31 of the resident key (by Parseval)
     int64_t level_issue_us = 0;    // host time the last level-split circuit spent issuing (TFHE_OPT_LEVEL_ISSUE_US)
     uint64_t near_tie_items = 0;   // items the margin guard recomputed (device err[1], read by sync_check)
     const char *last_br = "", *last_ks = "";
@@ -384,14 +386,24 @@ int key_fingerprint(tfhe_gpu_ctx *c, uint64_t &bk, uint64_t &ksk) {
 
 // Key admission of the fused arithmetic.  Its margin guard gives
 // the reference's words while the fused and the reference's pre-rounding values
-// differ by less than 1/4 — measured, not proven: 0.094 on keygen'd keys (BK
-// spectra up to 2^38.3), 0.125 on rows of random +-(2^31 - 1) (2^38.7), 0.19-0.22
-// where the spectrum concentrates (2^40.4-2^41; tests/test_oracle.py).  A key whose
-// largest BK spectrum component (reference scale) exceeds 2^39 is outside that
-// measured regime and runs the reference's expression trees instead
-// (TFHE_OPT_FUSED_ADMITTED reads the outcome).  A keygen'd component passes 2^39
-// with probability ~1e-22 (9.8 sigma), so honest keys always keep the fused path.
+// differ by less than 1/4 — measured, not proven.  Two rules, both on the device
+// key at load:
+//  - spectrum: the largest BK spectrum component (reference scale) <= 2^39 (round
+//    4: concentrated spectra, 2^40.4-2^41.3, reached gaps of 0.19-0.31);
+//  - row energy (round 5): every TRGSW row's RMS <= 0.65 x 2^31.  By Parseval the
+//    spectrum energy of a row is 2048 x its coefficient energy, so this bounds
+//    every row's L1 norm by 1024 x 0.65 x 2^31 and with it every pre-rounding value
+//    of the external product, |sum_i digit . row_i| <= 6 x 32 x 1024 x 0.65 x 2^31
+//    < 2^48 at the 128-bit set: below 2^48 an f64 ulp is at most 2^-5, half what it
+//    is above.  A hill-climbing search for the worst admitted key
+//    (tools/admission_search.py, profiles/r05_admission_search.json) finds gaps of
+//    at most 0.1875 under the spectrum rule alone (rows of +-(2^31 - 1), RMS 1) and
+//    0.125 under both.  Keygen'd rows have RMS 0.545-0.605 (8,400 rows of the
+//    seeded 128-bit key); exceeding 0.65 needs a 9.6-sigma row mean of a square.
+// A key outside either rule runs the reference's expression trees
+// (TFHE_OPT_FUSED_ADMITTED reads the outcome, TFHE_OPT_KEY_ROW_RMS_PPM the RMS).
 constexpr double FUSED_BK_SPECTRUM_MAX = 549755813888.0;  // 2^39
+constexpr double FUSED_BK_ROW_RMS_MAX = 0.65;             // x 2^31
 int key_admission(tfhe_gpu_ctx *c) {
     // refused until measured: a failure below (absmax launch, copy, sync) must not
     // leave the previous key's admission in place
@@ -400,13 +412,18 @@ int key_admission(tfhe_gpu_ctx *c) {
     auto *h = reinterpret_cast<volatile unsigned long long *>(c->h_err + 2);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, launch_absmax(c->d_bk, c->bk_bytes / sizeof(double), d, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_err + 2, d, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, launch_row_energy_max(c->d_bk, (size_t)c->P.n * 2 * c->P.L, d + 1, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_err + 2, d, 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const unsigned long long bits = *h;
-    double m;
+    const unsigned long long bits = h[0], ebits = h[1];
+    double m, e;
     std::memcpy(&m, (const void *)&bits, 8);
+    std::memcpy(&e, (const void *)&ebits, 8);
     c->bk_absmax = std::ldexp(m, 10);  // the device BK is the reference's spectrum x 2^-10 (k_bk_permute)
-    c->opts.key_fused_ok = c->bk_absmax <= FUSED_BK_SPECTRUM_MAX ? 1 : 0;  // NaN fails
+    // row energy: device spectrum energy x 2^20 = reference spectrum energy = 2048 x N x RMS^2
+    c->bk_row_rms = std::sqrt(std::ldexp(e, 20) / (2048.0 * c->P.N)) / 2147483648.0;
+    c->opts.key_fused_ok =
+        c->bk_absmax <= FUSED_BK_SPECTRUM_MAX && c->bk_row_rms <= FUSED_BK_ROW_RMS_MAX ? 1 : 0;  // NaN fails
     return TFHE_OK;
 }
 
@@ -1857,6 +1874,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_ARITH: *v = o.arith_strict == 1 ? TFHE_ARITH_REFERENCE : o.arith_strict == 2 ? TFHE_ARITH_FUSED_FORCED : TFHE_ARITH_AUTO; break;
     case TFHE_OPT_FUSED_ADMITTED: *v = o.key_fused_ok; break;
     case TFHE_OPT_LEVEL_ISSUE_US: *v = c->level_issue_us; break;
+    case TFHE_OPT_KEY_ROW_RMS_PPM: *v = (int64_t)std::llround(c->bk_row_rms * 1e6); break;
     case TFHE_OPT_BR_SYNC: *v = 1; break;
     case TFHE_OPT_BR_SPIN_CAP: *v = c->K.spin_cap; break;
     case TFHE_OPT_HOST_PIPELINE: *v = c->pipeline; break;
@@ -2014,6 +2032,7 @@ int broadcast_key(tfhe_gpu_ctx *c) {
             return fail(c, TFHE_ERR_HIP, "key broadcast: the copy on device " + std::to_string(s->device) +
                                              " differs from device " + std::to_string(c->device) + "'s");
         s->bk_absmax = c->bk_absmax;  // same bits, same admission
+        s->bk_row_rms = c->bk_row_rms;
         s->opts.key_fused_ok = c->opts.key_fused_ok;
         s->has_key = true;
     }

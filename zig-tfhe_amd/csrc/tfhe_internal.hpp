@@ -171,6 +171,9 @@ hipError_t launch_bk_permute(const KParams &P, const double *bk_ref, double *bkd
 // 64-bit fingerprint of bytes (a multiple of 16) at p into *out (device), async
 hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s);
 hipError_t launch_absmax(const double *p, size_t count, unsigned long long *out, hipStream_t s);
+// largest spectrum energy of one TRGSW row part (re^2 + im^2 over its N/2 values) over
+// `rows` device-layout BK rows (n * 2L), into *out (device, double bits), async
+hipError_t launch_row_energy_max(const double *bkd, size_t rows, unsigned long long *out, hipStream_t s);
 hipError_t launch_bk_unpermute(const KParams &P, const double *bkd, double *bk_ref, size_t rows,
                                hipStream_t s);
 

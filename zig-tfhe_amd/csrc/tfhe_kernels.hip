@@ -1824,6 +1824,40 @@ __global__ __launch_bounds__(256) void k_absmax_f64(const double2 *__restrict__ 
     if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
 
+// Largest energy (sum of squared re/im components) of one TRGSW row's spectrum
+// over the device BK (the key admission's row-energy rule):
+// one wave per (BK[i], row): lane t reads the row's 16-B words [q][part][t]
+// (device layout [i][row][q < 8][a|b][lane < 64] of double2), sums part a and
+// part b separately, and the wave's larger sum goes into one 64-bit atomic max
+// (non-negative doubles order like their bit patterns).
+__global__ __launch_bounds__(256) void k_row_energy_max(const double2 *__restrict__ bk, size_t rows,
+                                                        unsigned long long *out) {
+    const size_t r = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int t = threadIdx.x & 63;
+    if (r >= rows) return;
+    const double2 *row = bk + r * 1024;
+    double ea = 0.0, eb = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const double2 a = row[q * 128 + t], b = row[q * 128 + 64 + t];
+        ea += a.x * a.x + a.y * a.y;
+        eb += b.x * b.x + b.y * b.y;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        ea += __shfl_xor(ea, o);
+        eb += __shfl_xor(eb, o);
+    }
+    if (t == 0) atomicMax(out, (unsigned long long)__double_as_longlong(ea > eb ? ea : eb));
+}
+
+hipError_t launch_row_energy_max(const double *bkd, size_t rows, unsigned long long *out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(*out), s);
+    if (e != hipSuccess || rows == 0) return e;
+    hipLaunchKernelGGL(k_row_energy_max, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s,
+                       reinterpret_cast<const double2 *>(bkd), rows, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_absmax(const double *p, size_t count, unsigned long long *out, hipStream_t s) {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(*out), s);
     if (e != hipSuccess || count < 2) return e;

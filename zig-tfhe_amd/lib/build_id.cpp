@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "fbb4a7979347ae33"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "b797a328ef5233b6"; }

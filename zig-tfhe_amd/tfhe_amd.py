@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("TFHE_GPU_LIB") or os.path.join(HERE, "lib", "libtfhe_
 OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_groups": 5, "ks_sel_items": 6,
            "circuit_pack": 7, "twiddles": 8, "arith": 9, "br_sync": 10, "br_spin_cap": 11, "host_pipeline": 12,
            "circuit_split": 13}
-READONLY_OPTIONS = {"fused_admitted": 14, "level_issue_us": 15}  # tfhe_gpu_get_option only
+READONLY_OPTIONS = {"fused_admitted": 14, "level_issue_us": 15, "key_row_rms_ppm": 16}  # tfhe_gpu_get_option only
 OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 3, "ks_narrow": 0, "ks_item_groups": 0,
                    "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1, "br_spin_cap": 0,
                    "host_pipeline": 0, "circuit_split": 0}
