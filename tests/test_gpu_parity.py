@@ -726,11 +726,13 @@ def test_margin_guard_recomputes_near_ties(oracle, form):
 
 
 def test_key_admission_of_the_fused_arithmetic(oracle):
-    """DESIGN.md §6.1 key admission: keygen'd keys (BK spectra up to ~2^38.3) keep
-    the fused arithmetic; a loaded key whose BK spectrum reaches past 2^39 (one
-    row pair of constant 2^31 - 1 rows) is refused it and runs the reference's
-    trees, with the same words as the oracle; the refusal follows the key, not
-    the context (a later admitted key gets the fused arithmetic back)."""
+    """DESIGN.md §6.1 key admission: keygen'd keys (BK spectra up to ~2^38.3, row
+    RMS ~0.6 x 2^31) keep the fused arithmetic; a loaded key whose BK spectrum
+    reaches past 2^39 (one row of constant 2^31 - 1), or one of whose rows has an
+    RMS past 0.65 x 2^31 (+-(2^31 - 1), random signs: spectrum only 2^38.7), is
+    refused it and runs the reference's trees, with the same words as the
+    oracle; the refusal follows the key, not the context (a later admitted key
+    gets the fused arithmetic back)."""
     c, k = ctx_for(oracle, "80")
     assert c.get_option("fused_admitted") == 1
     p = k.p
@@ -751,6 +753,20 @@ def test_key_admission_of_the_fused_arithmetic(oracle):
         assert c2.last_kernels().split(" + ")[0].endswith("fused)")
         with pytest.raises(tfhe_amd.TfheError):
             c2.set_option("fused_admitted", 1)  # read-only
+        assert 545_000 < c2.get_option("key_row_rms_ppm") < 620_000  # keygen'd rows: RMS ~0.6 x 2^31
+        # round 5's row-energy rule: one row of +-(2^31 - 1) with random signs has a spectrum
+        # of ~2^38.7 (the round-4 rule admitted it) but RMS 1.0 > 0.65: refused, reference trees
+        g = rng(98)
+        bk2 = np.array(k.ck.bk, copy=True)
+        row = np.where(g.random(1024) < 0.5, (1 << 31) - 1, -((1 << 31) - 1)).astype(np.int64)
+        bk2[7, 2, 1] = oracle.ifft((row % (1 << 32)).astype(np.uint32))
+        assert np.abs(bk2[7, 2, 1]).max() < 2.0 ** 39
+        c2.load_cloud_key(k.ck.offset, k.ck.testvec, bk2, k.ck.ksk)
+        assert c2.get_option("fused_admitted") == 0
+        assert 999_000 < c2.get_option("key_row_rms_ppm") <= 1_000_000
+        want = np.array([oracle.blind_rotate(p, t, k.ck.testvec, bk2, k.ck.offset) for t in cts[:2]])
+        assert np.array_equal(c2.blind_rotate_batch(cts[:2]), want)
+        assert not c2.last_kernels().split(" + ")[0].endswith("fused)")
     finally:
         c2.close()
 
