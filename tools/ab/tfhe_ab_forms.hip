@@ -883,7 +883,12 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide2(
     }
 }
 
-// TFHE_OPT_BR_FORM 6 / 7 from the product launcher (launch_blind_rotate_form).
+hipError_t launch_blind_rotate_assist(const KParams &P, const DevTables &T, const uint8_t *ops, const uint32_t *in_a,
+                                      const uint32_t *in_b, const uint32_t *idx, const uint32_t *testvec,
+                                      const double2 *bk2, uint32_t *out, int out_mode, size_t B, hipStream_t s,
+                                      bool fused, const char **used);  // tfhe_ab_assist.hip
+
+// TFHE_OPT_BR_FORM 6 / 7 / 8 from the product launcher (launch_blind_rotate_form).
 hipError_t ab_launch_blind_rotate(int br_form, const KParams &P, const DevTables &T, const uint8_t *ops,
                                   const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                   const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B,
@@ -908,6 +913,8 @@ hipError_t ab_launch_blind_rotate(int br_form, const KParams &P, const DevTables
         }
         return hipGetLastError();
     }
+    if (br_form == 8)  // whole form, loader waves own polynomial b (tfhe_ab_assist.hip)
+        return launch_blind_rotate_assist(P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, fused, used);
     if (br_form == 7 && P.L == 3 && small) {  // latency form with split transforms
         const dim3 grid((unsigned)B), block(64 * BW_WAVES);
         if (fused) {

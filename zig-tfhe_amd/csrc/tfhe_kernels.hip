@@ -1308,8 +1308,8 @@ bool kernels_ab_build() { return false; }
 #endif
 
 // form: 'w' whole (default kernels: launch_whole_default), 'W' latency (one
-// item per 8-wave workgroup), 'o' octo (L = 1: 8 items per workgroup), 'd' /
-// '2' the A/B forms (TFHE_OPT_BR_FORM 6 / 7, A/B libraries only).
+// item per 8-wave workgroup), 'o' octo (L = 1: 8 items per workgroup), 'a' the
+// A/B forms (TFHE_OPT_BR_FORM 6-8, A/B libraries only).
 static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T, const uint8_t *ops,
                                            const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                            const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
@@ -1321,7 +1321,7 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
     // fused arithmetic in the exact-integer regime (SMALL) unless the
     // reference expression trees are requested (TFHE_OPT_ARITH)
     const bool fused = small && fused_allowed(O);
-    if (form == 'd' || form == '2') {
+    if (form == 'a') {  // an A/B form (TFHE_OPT_BR_FORM >= 6)
         if (!ab_launch_blind_rotate) return hipErrorInvalidValue;
         return ab_launch_blind_rotate(O.br_form, P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, fused,
                                       used);
@@ -1480,7 +1480,7 @@ static hipError_t launch_blind_rotate_forms(const KParams &P, const DevTables &T
                                             const uint32_t *testvec, const double *bkd, uint32_t *out, int out_mode,
                                             size_t B, hipStream_t s, const LaunchOpts &O, const char **used) {
     if (O.br_form) {  // forced form (TFHE_OPT_BR_FORM): the whole batch in one launch
-        const char f = O.br_form == 3 ? 'W' : O.br_form == 5 ? 'o' : O.br_form == 6 ? 'd' : O.br_form == 7 ? '2' : 'w';
+        const char f = O.br_form == 3 ? 'W' : O.br_form == 5 ? 'o' : O.br_form >= 6 ? 'a' : 'w';  // 6-8: A/B forms
         return launch_blind_rotate_form(P, T, ops, in_a, in_b, idx, testvec, bkd, out, out_mode, B, s, f, O, used);
     }
     const size_t round = BR_WAVES * device_cus(), tail = B % round;

@@ -1,1 +1,1 @@
-extern "C" const char *tfhe_gpu_build_id(void) { return "b797a328ef5233b6"; }
+extern "C" const char *tfhe_gpu_build_id(void) { return "f329aee4351f8cfd"; }
