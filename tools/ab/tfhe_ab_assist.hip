@@ -29,6 +29,13 @@
 
 namespace tfhe {
 
+#ifndef ASSIST_BWORK_FIRST  // 1: the b work before the wait for the next pair's refill (its 96-unit sleep)
+#define ASSIST_BWORK_FIRST 1
+#endif
+#ifndef ASSIST_GATE_PRIO  // issue priority of the gate waves (the loaders run at LOADER_PRIO = 0)
+#define ASSIST_GATE_PRIO 0
+#endif
+
 constexpr int BA_LDS_X = 512 * 16;  // per gate
 constexpr int BA_LDS_Y = 512 * 16;  // per gate (its loader's)
 constexpr int BA_LDS_AT = 1024 * 2;
@@ -148,12 +155,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
         for (uint32_t k = 0; k < pairs; k++) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of pair k landed
             counter_add(s_sync + (k & 1));
-            if (k + 1 < pairs) {
-                const uint32_t k1 = k + 1;
-                spin_until_ge<LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
-                issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048, s_bk + (k1 & 1) * 2048,
-                                    ltid);
-            }
+#if ASSIST_BWORK_FIRST  // the b work as soon as the own gate's fb is in, before the next DMA's wait
             if (k % L == 0) {
                 const uint32_t i = k / L;
                 if (i > 0) {  // step i - 1's b polynomial: fb from the gate, inverse, CMUX add
@@ -180,6 +182,41 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                 __builtin_amdgcn_sched_barrier(0);
                 counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
             }
+#endif
+            if (k + 1 < pairs) {
+                const uint32_t k1 = k + 1;
+                spin_until_ge<LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
+                issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048, s_bk + (k1 & 1) * 2048,
+                                    ltid);
+            }
+#if !ASSIST_BWORK_FIRST
+            if (k % L == 0) {
+                const uint32_t i = k / L;
+                if (i > 0) {  // step i - 1's b polynomial: fb from the gate, inverse, CMUX add
+                    spin_short(fb_ready + gi, i, spin_cap, fail);
+                    C2 f[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) f[q] = Y[q * 64 + t];
+                    inverse_one<FU>(f, Y, T, twist_t, t, accB, near);
+                }
+                wave_sync();  // the exchange's reads precede the copy's writes
+#pragma unroll
+                for (int m = 0; m < 16; m++) Y32[t + 64 * m] = accB[m];
+                wave_sync();
+                // step i's tB: X^{a~_i} acc_b - acc_b + offset, flipped (tmp_word)
+                const int at = __builtin_amdgcn_readfirstlane((int)s_at[i]);
+                uint32_t v[16], xb[16];
+                gather_rot_one(base, t, at, xb, v);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int m = 0; m < 16; m++) {
+                    const uint32_t sg = gather_sign(xb[m]), off_s = P.offset - sg;
+                    Y32[1024 + t + 64 * m] = tmp_word(v[m], sg, off_s, accB[m], msbs);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
+            }
+#endif
         }
         spin_short(fb_ready + gi, (uint32_t)n, spin_cap, fail);  // the last step's b polynomial
         {
@@ -205,6 +242,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
     }
 
     // ---- gate wave ----
+    if (ASSIST_GATE_PRIO) __builtin_amdgcn_s_setprio(ASSIST_GATE_PRIO);
     if (tid < 12) s_sync[tid] = 0u;
     for (int x = tid; x < 511; x += 256) s_tw[x] = TT.tw[x];
     for (int x = tid; x < 512; x += 256) s_twist[x] = TT.twist[x];

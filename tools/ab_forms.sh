@@ -3,12 +3,12 @@
 # latency forms, TFHE_OPT_BR_FORM 6 and 7) and tools/ab/tfhe_ab_assist.hip (the
 # loader-assist whole form, 8).  tfhe_gpu_create refuses it unless
 # TFHE_ALLOW_AB_BUILD=1; select it with TFHE_GPU_LIB:
-#   bash tools/ab_forms.sh [extra hipcc flags]
+#   [NAME=x] bash tools/ab_forms.sh [extra hipcc flags]   (NAME: tools/bin/lib_ab_x.so)
 #   TFHE_ALLOW_AB_BUILD=1 TFHE_GPU_LIB=$PWD/tools/bin/lib_ab.so python bench.py --opt br_form=6 ...
 set -e
 cd "$(dirname "$0")/.."
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Izig-tfhe_amd/csrc -DTFHE_AB_BUILD $*"
-O=tools/bin/ab_obj
+O=tools/bin/ab_obj${NAME:+_$NAME}
 mkdir -p $O
 $H -c -o $O/k.o zig-tfhe_amd/csrc/tfhe_kernels.hip &
 $H -mllvm -amdgpu-sched-strategy=max-memory-clause -c -o $O/w.o zig-tfhe_amd/csrc/tfhe_kernels_whole.hip &
@@ -18,5 +18,5 @@ $H -x hip -c -o $O/g.o zig-tfhe_amd/csrc/tfhe_gpu.cpp &
 wait
 printf 'extern "C" const char *tfhe_gpu_build_id(void) { return "ab-%s"; }\n' "$(cat $O/k.o $O/w.o $O/ab.o $O/as.o | sha256sum | cut -c1-13)" > $O/id.cpp
 g++ -O2 -fPIC -c -o $O/id.o $O/id.cpp
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/bin/lib_ab.so $O/k.o $O/w.o $O/ab.o $O/as.o $O/g.o $O/id.o
-echo "tools/bin/lib_ab.so"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/bin/lib_ab${NAME:+_$NAME}.so $O/k.o $O/w.o $O/ab.o $O/as.o $O/g.o $O/id.o
+echo "tools/bin/lib_ab${NAME:+_$NAME}.so"
