@@ -152,19 +152,25 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
         T.init(s_tw);  // pass-A twiddles from LDS (VGPRs): in SGPRs this loop failed to compile
         const C2 *twist_t = s_twist + t;
         const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_void_t *)Y32);  // acc_b copy: Y[0, 4 KB)
+        PhaseProf lp;  // tools/phase_prof.hip assist: 0 vmcnt + pub, 1 fb wait, 2 inverse b, 3 gather + tB, 4 refill wait + issue
+        lp.start();
         for (uint32_t k = 0; k < pairs; k++) {
+            lp.mark(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of pair k landed
             counter_add(s_sync + (k & 1));
 #if ASSIST_BWORK_FIRST  // the b work as soon as the own gate's fb is in, before the next DMA's wait
             if (k % L == 0) {
                 const uint32_t i = k / L;
                 if (i > 0) {  // step i - 1's b polynomial: fb from the gate, inverse, CMUX add
+                    lp.mark(1);
                     spin_short(fb_ready + gi, i, spin_cap, fail);
+                    lp.mark(2);
                     C2 f[8];
 #pragma unroll
                     for (int q = 0; q < 8; q++) f[q] = Y[q * 64 + t];
                     inverse_one<FU>(f, Y, T, twist_t, t, accB, near);
                 }
+                lp.mark(3);
                 wave_sync();  // the exchange's reads precede the copy's writes
 #pragma unroll
                 for (int m = 0; m < 16; m++) Y32[t + 64 * m] = accB[m];
@@ -181,10 +187,12 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
+                lp.mark(0);
             }
 #endif
             if (k + 1 < pairs) {
                 const uint32_t k1 = k + 1;
+                lp.mark(4);
                 spin_until_ge<LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
                 issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048, s_bk + (k1 & 1) * 2048,
                                     ltid);
@@ -193,12 +201,15 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
             if (k % L == 0) {
                 const uint32_t i = k / L;
                 if (i > 0) {  // step i - 1's b polynomial: fb from the gate, inverse, CMUX add
+                    lp.mark(1);
                     spin_short(fb_ready + gi, i, spin_cap, fail);
+                    lp.mark(2);
                     C2 f[8];
 #pragma unroll
                     for (int q = 0; q < 8; q++) f[q] = Y[q * 64 + t];
                     inverse_one<FU>(f, Y, T, twist_t, t, accB, near);
                 }
+                lp.mark(3);
                 wave_sync();  // the exchange's reads precede the copy's writes
 #pragma unroll
                 for (int m = 0; m < 16; m++) Y32[t + 64 * m] = accB[m];
@@ -215,6 +226,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
+                lp.mark(0);
             }
 #endif
         }
@@ -225,6 +237,11 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
             for (int q = 0; q < 8; q++) f[q] = Y[q * 64 + t];
             inverse_one<FU>(f, Y, T, twist_t, t, accB, near);
         }
+        lp.mark(5);
+#ifdef TFHE_PHASE_PROF
+        if (t == 0)
+            for (int q = 0; q < 6; q++) atomicAdd(&g_phase_cycles[8 + q], (unsigned long long)lp.acc[q]);
+#endif
         report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
         if (FU) near_tie_flag(P, near, g, valid);
         if (!valid) return;
@@ -267,7 +284,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
     const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_void_t *)X32);  // acc_a copy: X[0, 4 KB)
     int at_next = s_at[0];
     uint32_t near = NEAR_NONE, fail = 0;
+    PhaseProf pp;  // tools/phase_prof.hip assist: 0 gather + tmp, 1 pair 0 fft, 2 pub waits, 3 macs, 4 tB wait, 5 pairs 1-2 fft, 6 fb hand-off, 7 inverse a
+    pp.start();
     for (int i = 0; i < n; i++) {
+        pp.mark(0);
         const int at = __builtin_amdgcn_readfirstlane(at_next);
         uint32_t tA[16], xb[16];
         C2 tw0[8];
@@ -294,9 +314,11 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
             C2 d[2][8];
             double2 kpre[4];
             if (rp == 0) {
+                pp.mark(1);
                 load_digits_pair0_regs<FU>(d, tA, nullptr, L, P.bgbit, tw0);  // rows 0, 1: a's levels 0, 1
             } else {
                 if (rp == 1) {  // tB(i) from the loader, packed with a's level 2 (load_digits_pair_tbx)
+                    pp.mark(4);
                     spin_short(tb_ready + gi, (uint32_t)i + 1u, spin_cap, fail);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -304,27 +326,37 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                         tbx[m] = __builtin_amdgcn_ubfe(tA[m], 32 - L * P.bgbit, P.bgbit) |
                                  (Y32[1024 + t + 64 * m] & ~((1u << P.bgbit) - 1u));
                 }
+                pp.mark(5);
                 load_digits_pair_tbx<FU>(d, tbx, rp, P.bgbit, twist_t);
             }
             fft512_x2<false, true, FU>(d, X, T, t);
             const uint32_t k = (uint32_t)(L * i + rp);
+            pp.mark(2);
             wait_pair_first_group(s_sync, s_bk + (k & 1) * 2048 + t, k, spin_cap, fail, kpre);
             __builtin_amdgcn_sched_barrier(0);
+            pp.mark(3);
             mac_pair_lds<FU>(fa, fb, d[0], d[1], s_bk + (k & 1) * 2048, t, kpre);
             __builtin_amdgcn_sched_barrier(0);
             counter_add(s_sync + 2 + (k & 1));
         }
         // hand fb to the loader (it read tB(i) from Y before: this wave's reads came first)
+        pp.mark(6);
 #pragma unroll
         for (int q = 0; q < 8; q++) Y[q * 64 + t] = fb[q];
         __builtin_amdgcn_sched_barrier(0);
         counter_add(fb_ready + gi);
+        pp.mark(7);
         inverse_one<FU>(fa, X, T, twist_t, t, accA, near);
         wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) X32[t + 64 * m] = accA[m];
         wave_sync();
     }
+    pp.mark(0);
+#ifdef TFHE_PHASE_PROF
+    if (t == 0)
+        for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[q], (unsigned long long)pp.acc[q]);
+#endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU) near_tie_flag(P, near, g, valid);
     if (!valid) return;

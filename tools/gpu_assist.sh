@@ -16,3 +16,8 @@ for r in $(seq $N); do
     echo -n "$v: "; timeout -k 10 120 env BR_FORM=assist $(ab $v) python tools/ab_assist_check.py time 40 2>/dev/null | tail -1 | cut -c1-90 || exit 2
   done
 done
+# phase profiles (s_memtime marks; tools/phase_prof.hip built with -DTFHE_PHASE_PROF)
+if [ -x tools/bin/phase_prof ]; then
+  timeout -k 10 120 tools/bin/phase_prof 1024 whole 2>&1 | tail -16
+  timeout -k 10 120 tools/bin/phase_prof 1024 assist 2>&1 | tail -16
+fi

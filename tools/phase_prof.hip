@@ -6,6 +6,7 @@
 //         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
 #include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
 #include "../zig-tfhe_amd/csrc/tfhe_kernels_whole.hip"
+#include "ab/tfhe_ab_assist.hip"  // the loader-assist A/B form (mode "assist")
 
 #include <cstdio>
 #include <cstdlib>
@@ -52,7 +53,15 @@ int main(int argc, char **argv) {
         LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
         const char *form = argc > 2 ? argv[2] : "whole";
         O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
-        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
+        const bool assist = form[0] == 'a';
+        if (assist) {
+            KParams Q = P;
+            Q.tie_flags = nullptr;
+            CK(launch_blind_rotate_assist(Q, T, nullptr, d_in, nullptr, nullptr, d_tv, reinterpret_cast<const double2 *>(d_bk),
+                                          d_out, BR_OUT_LV1, B, 0, true, nullptr));
+        } else {
+            CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
+        }
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -70,6 +79,19 @@ int main(int argc, char **argv) {
                 for (int w = 0; w < 8; w++) printf(" %8.1f", c[w * 16 + k] / (double)B / P.n);
                 printf("\n");
             }
+            continue;
+        }
+        if (assist) {  // gates [0, 8), loaders [8, 14), per wave-step
+            const char *gn[8] = {"gate: gather+tmp", "gate: pair0 digits+fft", "gate: pub waits", "gate: macs",
+                                 "gate: tB wait+tbx", "gate: pairs1-2 digits+fft", "gate: fb hand-off", "gate: inverse a+store"};
+            const char *ln[6] = {"loader: vmcnt+pub", "loader: fb wait", "loader: inverse b", "loader: acc_b+gather+tB",
+                                 "loader: refill wait+issue", "loader: tail"};
+            double tot = 0;
+            for (int k = 0; k < 8; k++) tot += c[k];
+            printf("rep %d: %.3f ms (%zu gates, assist form); s_memtime ticks per wave-step:\n", rep, ms, B);
+            for (int k = 0; k < 8; k++) printf("  %-26s %9.1f  %5.1f%%\n", gn[k], c[k] / (double)B / P.n, 100.0 * c[k] / tot);
+            printf("  %-26s %9.1f\n", "gate total", tot / B / P.n);
+            for (int k = 0; k < 6; k++) printf("  %-26s %9.1f\n", ln[k], c[8 + k] / (double)B / P.n);
             continue;
         }
         const char *nm[8] = {"tmp", "fwd-fft(pairs)", "slot wait", "mac", "counter add", "inverse+add", "tail", "dma-issue"};
