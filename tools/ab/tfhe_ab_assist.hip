@@ -35,6 +35,15 @@ namespace tfhe {
 #ifndef ASSIST_GATE_PRIO  // issue priority of the gate waves (the loaders run at LOADER_PRIO = 0)
 #define ASSIST_GATE_PRIO 0
 #endif
+#ifndef ASSIST_GATE_EX2LDS  // 1: the gate's single inverse transform does exchange 2 through LDS, not registers
+#define ASSIST_GATE_EX2LDS 0
+#endif
+#ifndef ASSIST_LOADER_EX2LDS  // the same for the loader's inverse of b
+#define ASSIST_LOADER_EX2LDS 0
+#endif
+#ifndef ASSIST_LOADER_WORK_PRIO  // issue priority of a loader wave during its b work (0: LOADER_PRIO throughout)
+#define ASSIST_LOADER_WORK_PRIO 0
+#endif
 
 constexpr int BA_LDS_X = 512 * 16;  // per gate
 constexpr int BA_LDS_Y = 512 * 16;  // per gate (its loader's)
@@ -67,12 +76,12 @@ DEV void gather_rot_one(uint32_t base, int t, int at, uint32_t *xb, uint32_t *v)
 // Inverse transform of ONE accumulated spectrum (fft1024), untwist, guarded
 // conversion and the CMUX add into acc (lane-local); exchange 1 through xb,
 // exchange 2 in registers (the single-transform fft512).
-template <bool FU>
+template <bool FU, bool EX2LDS = false>
 DEV void inverse_one(const C2 *f, C2 *xb, const LdsTw &T, const C2 *twist_t, int t, uint32_t *acc, uint32_t &near) {
     C2 e[1][8];
 #pragma unroll
     for (int q = 0; q < 8; q++) e[0][q] = f[br3(q)];
-    fft512<1, true, FU, LdsTw, false>(e, xb, T, t);
+    fft512<1, true, FU, LdsTw, EX2LDS>(e, xb, T, t);
     uint32_t nq[2] = {NEAR_NONE, NEAR_NONE};
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -168,7 +177,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                     C2 f[8];
 #pragma unroll
                     for (int q = 0; q < 8; q++) f[q] = Y[q * 64 + t];
-                    inverse_one<FU>(f, Y, T, twist_t, t, accB, near);
+                    if (ASSIST_LOADER_WORK_PRIO) __builtin_amdgcn_s_setprio(ASSIST_LOADER_WORK_PRIO);
+                    inverse_one<FU, ASSIST_LOADER_EX2LDS>(f, Y, T, twist_t, t, accB, near);
                 }
                 lp.mark(3);
                 wave_sync();  // the exchange's reads precede the copy's writes
@@ -187,6 +197,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
+                if (ASSIST_LOADER_WORK_PRIO) __builtin_amdgcn_s_setprio(LOADER_PRIO);
                 lp.mark(0);
             }
 #endif
@@ -207,7 +218,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                     C2 f[8];
 #pragma unroll
                     for (int q = 0; q < 8; q++) f[q] = Y[q * 64 + t];
-                    inverse_one<FU>(f, Y, T, twist_t, t, accB, near);
+                    if (ASSIST_LOADER_WORK_PRIO) __builtin_amdgcn_s_setprio(ASSIST_LOADER_WORK_PRIO);
+                    inverse_one<FU, ASSIST_LOADER_EX2LDS>(f, Y, T, twist_t, t, accB, near);
                 }
                 lp.mark(3);
                 wave_sync();  // the exchange's reads precede the copy's writes
@@ -226,6 +238,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
+                if (ASSIST_LOADER_WORK_PRIO) __builtin_amdgcn_s_setprio(LOADER_PRIO);
                 lp.mark(0);
             }
 #endif
@@ -235,7 +248,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
             C2 f[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) f[q] = Y[q * 64 + t];
-            inverse_one<FU>(f, Y, T, twist_t, t, accB, near);
+            inverse_one<FU, ASSIST_LOADER_EX2LDS>(f, Y, T, twist_t, t, accB, near);
         }
         lp.mark(5);
 #ifdef TFHE_PHASE_PROF
@@ -346,7 +359,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
         __builtin_amdgcn_sched_barrier(0);
         counter_add(fb_ready + gi);
         pp.mark(7);
-        inverse_one<FU>(fa, X, T, twist_t, t, accA, near);
+        inverse_one<FU, ASSIST_GATE_EX2LDS>(fa, X, T, twist_t, t, accA, near);
         wave_sync();
 #pragma unroll
         for (int m = 0; m < 16; m++) X32[t + 64 * m] = accA[m];

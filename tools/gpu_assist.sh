@@ -17,7 +17,7 @@ for r in $(seq $N); do
   done
 done
 # phase profiles (s_memtime marks; tools/phase_prof.hip built with -DTFHE_PHASE_PROF)
-if [ -x tools/bin/phase_prof ]; then
+if [ -x tools/bin/phase_prof ] && [ -z "$NOPROF" ]; then
   timeout -k 10 120 tools/bin/phase_prof 1024 whole 2>&1 | tail -16
   timeout -k 10 120 tools/bin/phase_prof 1024 assist 2>&1 | tail -16
 fi
