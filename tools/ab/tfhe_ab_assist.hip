@@ -38,8 +38,11 @@ namespace tfhe {
 #ifndef ASSIST_GATE_EX2LDS  // 1: the gate's single inverse transform does exchange 2 through LDS, not registers
 #define ASSIST_GATE_EX2LDS 0
 #endif
-#ifndef ASSIST_LOADER_EX2LDS  // the same for the loader's inverse of b
-#define ASSIST_LOADER_EX2LDS 0
+#ifndef ASSIST_LOADER_EX2LDS  // the same for the loader's inverse of b (1: 6.08-6.09 vs 6.14-6.15 ms)
+#define ASSIST_LOADER_EX2LDS 1
+#endif
+#ifndef ASSIST_LOADER_SLEEP  // the loaders' poll period while waiting to refill a slot (whole form: 96)
+#define ASSIST_LOADER_SLEEP 96
 #endif
 #ifndef ASSIST_LOADER_WORK_PRIO  // issue priority of a loader wave during its b work (0: LOADER_PRIO throughout)
 #define ASSIST_LOADER_WORK_PRIO 0
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
         const int ltid = tid - 64 * BR_WAVES;
         __builtin_amdgcn_s_setprio(LOADER_PRIO);
         const size_t stride = (size_t)L * 2048;
-        const uint32_t loader_cap = spin_cap / LOADER_SLEEP > 0 ? spin_cap / LOADER_SLEEP : 1u;
+        const uint32_t loader_cap = spin_cap / ASSIST_LOADER_SLEEP > 0 ? spin_cap / ASSIST_LOADER_SLEEP : 1u;
         uint32_t near = NEAR_NONE, fail = 0;
         issue_bk_pair_async(bkd, s_bk, ltid);  // pair 0 into slot 0
         // b~ of this wave's item (trgsw.zig:312), as the gate computes it
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
             if (k + 1 < pairs) {
                 const uint32_t k1 = k + 1;
                 lp.mark(4);
-                spin_until_ge<LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
+                spin_until_ge<ASSIST_LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
                 issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048, s_bk + (k1 & 1) * 2048,
                                     ltid);
             }
