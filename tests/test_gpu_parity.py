@@ -134,7 +134,10 @@ def test_blind_rotate_vs_oracle(oracle, pname, B, form):
         assert np.array_equal(c.blind_rotate_batch(cts), want)
         # fused arithmetic only where the external product is exact (SMALL)
         assert c.last_kernels().split(" + ")[0].endswith("fused)") == (pname != "uint4" and not form.endswith("reference"))
-        prefix = {"whole": "k_blind_rotate<", "octo": "k_blind_rotate_octo<", "wide": "k_blind_rotate_wide<"}
+        # the whole form at L = 3 with the fused arithmetic is the loader-assist kernel
+        assist = form == "whole" and pname != "uint4"
+        prefix = {"whole": "k_blind_rotate_assist<" if assist else "k_blind_rotate<", "octo": "k_blind_rotate_octo<",
+                  "wide": "k_blind_rotate_wide<"}
         assert c.last_kernels().startswith(prefix[form.split("-")[0]])
         assert np.array_equal(c.blind_rotate_batch(cts5), want5)
 
@@ -651,7 +654,7 @@ def test_options_validation_and_report(oracle):
         assert c.last_kernels() == "k_blind_rotate_wide<3,true,false> (latency form) + " + gemm
     with c.options(br_form="whole"):
         c.bootstrap_batch(cts)
-        assert c.last_kernels() == "k_blind_rotate<3,true,true> (whole form, fused) + " + gemm
+        assert c.last_kernels() == "k_blind_rotate_assist<true> (whole form, loader waves own polynomial b, fused) + " + gemm
     with c.options(ks_form=0):
         c.bootstrap_batch(cts)
         assert c.last_kernels().endswith("k_key_switch_lanes<9,2,32,4,1>")
@@ -670,7 +673,7 @@ def test_whole_form_full_and_ragged_headline_batches(oracle):
         ops = np.zeros(Bn, np.uint8)
         with c.options(br_form="whole"):
             fused = c.gate_batch(ops, A, B)
-            assert c.last_kernels().startswith("k_blind_rotate<3,true,true>")
+            assert c.last_kernels().startswith("k_blind_rotate_assist<true>")
         with c.options(br_form="whole", arith=tfhe_amd.ARITH_REFERENCE):
             ref = c.gate_batch(ops, A, B)
             assert c.last_kernels().startswith("k_blind_rotate<3,true,false>")

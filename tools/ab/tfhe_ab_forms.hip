@@ -2,11 +2,13 @@
 // buildable for further A/B work but NOT part of the product library
 // (VERDICT r04 item 3).  tools/ab_forms.sh links this unit into an A/B library
 // (tools/bin/lib_ab.so, compiled with TFHE_AB_BUILD: tfhe_gpu_create refuses
-// it unless TFHE_ALLOW_AB_BUILD=1), where TFHE_OPT_BR_FORM 6 (duo) and 7
-// (split-transform latency form) reach these kernels through the product
-// launcher's weak hook ab_launch_blind_rotate.  Measurements: DESIGN.md §4.2
-// (wide2: 109.4-109.8 vs 99.9 ms per 16-bit adder) and §4.3d (duo: 7.93-8.05
-// vs 6.12-6.18 ms per 1,024 gates).  The development switches below (TFHE_KO_*,
+// it unless TFHE_ALLOW_AB_BUILD=1), where TFHE_OPT_BR_FORM 6 (duo), 7
+// (split-transform latency form) and 8 (round 4's whole form at L = 3, whose
+// loader waves only issue DMAs: the reference point of the round-5 loader
+// assist) reach these kernels through the product launcher's weak hook
+// ab_launch_blind_rotate.  Measurements: DESIGN.md §4.2 (wide2: 109.4-109.8 vs
+// 99.9 ms per 16-bit adder), §4.3d (duo: 7.93-8.05 vs 6.12-6.18 ms per 1,024
+// gates), §4.1b (assist).  The development switches below (TFHE_KO_*,
 // TFHE_DUO_*) apply to this unit only.
 #include <cmath>
 
@@ -883,11 +885,6 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide2(
     }
 }
 
-hipError_t launch_blind_rotate_assist(const KParams &P, const DevTables &T, const uint8_t *ops, const uint32_t *in_a,
-                                      const uint32_t *in_b, const uint32_t *idx, const uint32_t *testvec,
-                                      const double2 *bk2, uint32_t *out, int out_mode, size_t B, hipStream_t s,
-                                      bool fused, const char **used);  // tfhe_ab_assist.hip
-
 // TFHE_OPT_BR_FORM 6 / 7 / 8 from the product launcher (launch_blind_rotate_form).
 hipError_t ab_launch_blind_rotate(int br_form, const KParams &P, const DevTables &T, const uint8_t *ops,
                                   const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
@@ -913,8 +910,13 @@ hipError_t ab_launch_blind_rotate(int br_form, const KParams &P, const DevTables
         }
         return hipGetLastError();
     }
-    if (br_form == 8)  // whole form, loader waves own polynomial b (tfhe_ab_assist.hip)
-        return launch_blind_rotate_assist(P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, fused, used);
+    if (br_form == 8 && P.L == 3 && small && fused) {  // round 4's whole form at L = 3 (loader waves issue DMAs only)
+        const dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(64 * BR_WAVES * 2);
+        hipLaunchKernelGGL((k_blind_rotate<3, true, true>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec, bk2,
+                           out, out_mode, B);
+        if (used) *used = "k_blind_rotate<3,true,true> (whole form without loader assist, fused)";
+        return hipGetLastError();
+    }
     if (br_form == 7 && P.L == 3 && small) {  // latency form with split transforms
         const dim3 grid((unsigned)B), block(64 * BW_WAVES);
         if (fused) {

@@ -6,7 +6,6 @@
 //         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
 #include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
 #include "../zig-tfhe_amd/csrc/tfhe_kernels_whole.hip"
-#include "ab/tfhe_ab_assist.hip"  // the loader-assist A/B form (mode "assist")
 
 #include <cstdio>
 #include <cstdlib>
@@ -53,15 +52,8 @@ int main(int argc, char **argv) {
         LaunchOpts O;  // form from argv[2]: "wide" = latency form, else the whole form
         const char *form = argc > 2 ? argv[2] : "whole";
         O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
-        const bool assist = form[0] == 'a';
-        if (assist) {
-            KParams Q = P;
-            Q.tie_flags = nullptr;
-            CK(launch_blind_rotate_assist(Q, T, nullptr, d_in, nullptr, nullptr, d_tv, reinterpret_cast<const double2 *>(d_bk),
-                                          d_out, BR_OUT_LV1, B, 0, true, nullptr));
-        } else {
-            CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
-        }
+        const bool assist = O.br_form == 1;  // L = 3 fused: the whole form with loader assist
+        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));

@@ -1375,7 +1375,7 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
         if (used) {
             static const char *names[4] = {"", "k_blind_rotate<1,true,true> (whole form, fused)",
                                            "k_blind_rotate<2,true,true> (whole form, fused)",
-                                           "k_blind_rotate<3,true,true> (whole form, fused)"};
+                                           "k_blind_rotate_assist<true> (whole form, loader waves own polynomial b, fused)"};
             *used = P.L >= 1 && P.L <= 3 ? names[P.L] : "";
         }
         return e;
