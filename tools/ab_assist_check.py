@@ -1,6 +1,7 @@
-"""A/B check of the loader-assist whole form (TFHE_OPT_BR_FORM 8, tools/ab/tfhe_ab_assist.hip)
-in the A/B library: words against the product's default whole form and the oracle, every
-idle-slot count, the three output modes; then alternating timing against the product library.
+"""A/B check of the whole form at L = 3 (since round 5 the loader-assist kernel,
+k_blind_rotate_assist) against round 4's whole form (A/B form 8 "plain",
+tools/ab/tfhe_ab_forms.hip) and the oracle: every idle-slot count, the three output
+modes; then timing of one form (BR_FORM=whole|plain|auto).
 Run with TFHE_ALLOW_AB_BUILD=1 TFHE_GPU_LIB=tools/bin/lib_ab.so.
 
     python tools/ab_assist_check.py parity
@@ -36,31 +37,31 @@ def parity():
     g = np.random.default_rng(5)
     cts = u32rand(g, 9, p.n + 1)
     want = np.array([o.blind_rotate(p, t, ck.testvec, ck.bk, ck.offset) for t in cts[:3]])
-    with c.options(br_form="assist"):
+    with c.options(br_form="whole"):
         got = c.blind_rotate_batch(cts[:3])
         print("kernel:", c.last_kernels())
     assert np.array_equal(got, want), "assist TRLWE != oracle"
-    with c.options(br_form="whole"):
+    with c.options(br_form="plain"):
         ref9 = c.blind_rotate_batch(cts)
-    with c.options(br_form="assist"):
+    with c.options(br_form="whole"):
         for B in range(1, 10):
             assert np.array_equal(c.blind_rotate_batch(cts[:B]), ref9[:B]), f"idle slots B={B}"
-    print("TRLWE outputs bit-exact (oracle on 3, whole form at B = 1..9)")
+    print("TRLWE outputs bit-exact (oracle on 3, round 4's whole form at B = 1..9)")
     sk = tfhe_amd.SecretKey(c.params, k0, k1)
     a, b = g.integers(0, 2, 1024).astype(np.uint8), g.integers(0, 2, 1024).astype(np.uint8)
     A, Bc = sk.encrypt_bool(a, seed0=1), sk.encrypt_bool(b, seed0=5000)
     ops = g.integers(0, 10, 1024).astype(np.uint8)
-    with c.options(br_form="whole"):
+    with c.options(br_form="plain"):
         ref = c.gate_batch(ops, A, Bc)
         ref2 = c.bootstrap_without_key_switch_batch(A[:37])
-    with c.options(br_form="assist"):
+    with c.options(br_form="whole"):
         out = c.gate_batch(ops, A, Bc)
         out2 = c.bootstrap_without_key_switch_batch(A[:37])
     assert np.array_equal(out, ref), f"gate batch: {(out != ref).any(axis=1).sum()} gates differ"
     assert np.array_equal(out2, ref2)
     idx = np.array([0, 513, 1023])
     assert np.array_equal(out[idx], o.gate_batch(p, ops[idx], A[idx], Bc[idx], ck, threads=3))
-    print("1,024 mixed gates and 37 bootstraps without key switch: identical to the whole form; oracle sample ok")
+    print("1,024 mixed gates and 37 bootstraps without key switch: identical to round 4's whole form; oracle sample ok")
     print("near-tie items recomputed:", c.near_tie_items())
     c.close()
 

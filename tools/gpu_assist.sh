@@ -1,6 +1,7 @@
-# A/B of the loader-assist whole form (tools/ab/tfhe_ab_assist.hip, TFHE_OPT_BR_FORM 8 in
-# tools/bin/lib_ab_<variant>.so): parity of the first variant (bounded waits), then alternating
-# timing of every variant against the product library's default whole form.
+# A/B of whole-form variants built as tools/bin/lib_ab_<variant>.so (tools/ab_forms.sh NAME=...):
+# parity of the first variant's whole form against round 4's (A/B form 8 "plain") and the oracle
+# (bounded waits), then alternating timing of every variant's whole form against the product
+# library's default.  (Round 5 used it for the loader-assist form before it became the default.)
 #   bash tools/gpu_assist.sh TAG ROUNDS VARIANT...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -13,7 +14,7 @@ grep -v amdgpu.ids gpurun_out/$TAG.parity.log
 for r in $(seq $N); do
   timeout -k 10 120 python tools/ab_assist_check.py time 40 2>/dev/null | tail -1 | cut -c1-90 || exit 2
   for v in "$@"; do
-    echo -n "$v: "; timeout -k 10 120 env BR_FORM=assist $(ab $v) python tools/ab_assist_check.py time 40 2>/dev/null | tail -1 | cut -c1-90 || exit 2
+    echo -n "$v: "; timeout -k 10 120 env BR_FORM=whole $(ab $v) python tools/ab_assist_check.py time 40 2>/dev/null | tail -1 | cut -c1-90 || exit 2
   done
 done
 # phase profiles (s_memtime marks; tools/phase_prof.hip built with -DTFHE_PHASE_PROF)
