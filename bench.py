@@ -215,8 +215,9 @@ def rooflines(p, B, params, br_avg_s, kernel):
             "arithmetic": "fused multiply-add (exact-integer regime, DESIGN.md §6)" if fused else "reference expression trees",
             "reference_tree_f64_ops_per_cmux": f64_ops_per_cmux(p.L)}
     if pmc:
-        roof["pmc"] = {k: pmc[k] for k in ("valu_f64_insts_per_launch", "valu_insts_per_gate_wave_per_cmux",
-                                           "lds_insts_per_gate_wave_per_cmux", "wait_any_frac_gate_waves")
+        roof["pmc"] = {k: pmc[k] for k in ("valu_f64_insts_per_launch", "valu_insts_per_item_per_cmux",
+                                           "lds_insts_per_item_per_cmux", "valu_insts_per_gate_wave_per_cmux",
+                                           "lds_insts_per_gate_wave_per_cmux", "wait_any_frac_all_waves")
                        if k in pmc}
         f64_insts = pmc.get("valu_f64_insts_per_launch", 0) + pmc.get("valu_fma_f64_insts_per_launch", 0)
         if f64_insts:

@@ -62,10 +62,15 @@ def main():
     if "SQ_INSTS_VALU_ADD_F64" in per:
         rec["valu_f64_insts_per_launch"] = per["SQ_INSTS_VALU_ADD_F64"] + per.get("SQ_INSTS_VALU_MUL_F64", 0.0)
         rec["valu_fma_f64_insts_per_launch"] = per.get("SQ_INSTS_VALU_FMA_F64", 0.0)
-    if "SQ_INSTS_VALU" in per:  # gate waves = batch (the loader waves issue few VALU instructions)
-        rec["valu_insts_per_gate_wave_per_cmux"] = round(per["SQ_INSTS_VALU"] / batch / n, 1)
+    # per item (= per gate wave and its loader wave): since round 5 the L = 3 whole form's loader
+    # waves run polynomial b's inverse transform, conversion and gather, so the
+    # loader's VALU is part of the item's stream; the gate wave's own share is a static count
+    # (tools/isa_stats.py, profiles/r05_isa_census.txt).  The *_per_gate_wave_* keys of earlier
+    # files are the same ratio (their loader waves issued almost no VALU).
+    if "SQ_INSTS_VALU" in per:
+        rec["valu_insts_per_item_per_cmux"] = round(per["SQ_INSTS_VALU"] / batch / n, 1)
     if "SQ_INSTS_LDS" in per:
-        rec["lds_insts_per_gate_wave_per_cmux"] = round(per["SQ_INSTS_LDS"] / batch / n, 1)
+        rec["lds_insts_per_item_per_cmux"] = round(per["SQ_INSTS_LDS"] / batch / n, 1)
     if "SQ_WAIT_ANY" in per and "SQ_WAVE_CYCLES" in per:
         rec["wait_any_frac_all_waves"] = round(per["SQ_WAIT_ANY"] / per["SQ_WAVE_CYCLES"], 4)
     if "SQ_ACTIVE_INST_VALU" in per and "SQ_WAVE_CYCLES" in per:
