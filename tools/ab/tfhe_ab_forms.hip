@@ -885,7 +885,13 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide2(
     }
 }
 
-// TFHE_OPT_BR_FORM 6 / 7 / 8 from the product launcher (launch_blind_rotate_form).
+hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, const KParams &P, const DevTables &T,
+                                const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
+                                const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B,
+                                const char **used);  // tfhe_ab_assist_dev.hip
+
+// TFHE_OPT_BR_FORM 6 / 7 / 8 (and 9 + VAR: tfhe_ab_assist_dev.hip) from the product launcher
+// (launch_blind_rotate_form).
 hipError_t ab_launch_blind_rotate(int br_form, const KParams &P, const DevTables &T, const uint8_t *ops,
                                   const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                   const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B,
@@ -916,6 +922,11 @@ hipError_t ab_launch_blind_rotate(int br_form, const KParams &P, const DevTables
                            out, out_mode, B);
         if (used) *used = "k_blind_rotate<3,true,true> (whole form without loader assist, fused)";
         return hipGetLastError();
+    }
+    if (br_form >= 9 && P.L == 3 && small && fused) {  // development copies of the assist form
+        const dim3 grid((unsigned)((B + BR_WAVES - 1) / BR_WAVES)), block(64 * BR_WAVES * 2);
+        return ab_launch_assist_dev(br_form - 9, grid, block, s, P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode,
+                                    B, used);
     }
     if (br_form == 7 && P.L == 3 && small) {  // latency form with split transforms
         const dim3 grid((unsigned)B), block(64 * BW_WAVES);
