@@ -2,7 +2,9 @@
 // (csrc/tfhe_kernels_whole.hip, k_blind_rotate_assist) for A/B work in the A/B library only
 // (tools/ab_forms.sh).  TFHE_OPT_BR_FORM 9 + VAR: VAR 0 = the product kernel as is (control),
 // VAR 1 = knock-out timing build: pair 2 runs ONE forward transform (row 4) and reuses it for
-// row 5 (wrong words; the upper bound of moving row 5's transform off the gate wave).
+// row 5 (wrong words; the upper bound of moving row 5's transform off the gate wave),
+// VAR 2 = the loader wave also transforms row 5 (b's last level) from its tB words and hands
+// the spectrum to the gate through Y (counters tb_read, r5_ready); same arithmetic and words.
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
 namespace tfhe {
@@ -10,7 +12,7 @@ namespace tfhe {
 constexpr int BAD_LDS_X = 512 * 16;  // per gate
 constexpr int BAD_LDS_Y = 512 * 16;  // per gate (its loader's)
 constexpr int BAD_LDS_AT = 1024 * 2;
-constexpr int BAD_LDS_SYNC = 64;  // pub[2] done[2] fb_ready[4] tb_ready[4]
+constexpr int BAD_LDS_SYNC = 128;  // pub[2] done[2] fb_ready[4] tb_ready[4] tb_read[4] r5_ready[4]
 constexpr int BAD_X_AT = BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;
 constexpr int BAD_Y_AT = BAD_X_AT + BR_WAVES * BAD_LDS_X;
 constexpr int BAD_AT_AT = BAD_Y_AT + BR_WAVES * BAD_LDS_Y;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     uint32_t *X32 = reinterpret_cast<uint32_t *>(X), *Y32 = reinterpret_cast<uint32_t *>(Y);
     uint16_t *s_at = reinterpret_cast<uint16_t *>(smem + BAD_AT_AT + gi * BAD_LDS_AT);
     uint32_t *s_sync = reinterpret_cast<uint32_t *>(smem + BAD_LDS_TOTAL - BAD_LDS_SYNC);
-    uint32_t *fb_ready = s_sync + 4, *tb_ready = s_sync + 8;
+    uint32_t *fb_ready = s_sync + 4, *tb_ready = s_sync + 8, *tb_read = s_sync + 12, *r5_ready = s_sync + 16;
     if (lds_layout_bad(smem)) {
         if (tid == 0) __hip_atomic_fetch_or(P.err, (uint32_t)DEV_ERR_LDS_LAYOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
@@ -125,10 +127,15 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
         const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_void_t *)Y32);  // acc_b copy: Y[0, 4 KB)
         PhaseProf lp;  // tools/phase_prof.hip assist: 0 vmcnt + pub, 1 fb wait, 2 inverse b, 3 gather + tB, 4 refill wait + issue
         lp.start();
+        bool pre_pub = false;  // VAR 2: pair k was published inside the row-5 block
         for (uint32_t k = 0; k < pairs; k++) {
             lp.mark(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of pair k landed
-            counter_add(s_sync + (k & 1));
+            if (!pre_pub) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of pair k landed
+                counter_add(s_sync + (k & 1));
+            }
+            pre_pub = false;
+            uint32_t tbw[16];  // VAR 2: step i's tB words, kept for row 5's digits
             // the b work as soon as the own gate's fb is in, before the wait for the next refill (with its
             // 96-unit sleep): 6.15 vs 6.65 ms after it
             if (k % L == 0) {
@@ -155,7 +162,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
 #pragma unroll
                 for (int m = 0; m < 16; m++) {
                     const uint32_t sg = gather_sign(xb[m]), off_s = P.offset - sg;
-                    Y32[1024 + t + 64 * m] = tmp_word(v[m], sg, off_s, accB[m], msbs);
+                    tbw[m] = tmp_word(v[m], sg, off_s, accB[m], msbs);
+                    Y32[1024 + t + 64 * m] = tbw[m];
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
@@ -167,6 +175,31 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                 spin_until_ge<LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
                 issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048, s_bk + (k1 & 1) * 2048,
                                     ltid);
+                if (VAR == 2 && k % L == 0) {
+                    // row 5 (b's last level) of step i: digits from the tB words, forward transform through Y
+                    // once the gate has read tB out of it, spectrum handed over in Y (r5_ready); pair k + 1
+                    // is published first (its DMA landed under the digits)
+                    const uint32_t i = k / L;
+                    C2 e[1][8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const int m = br3(q);
+                        e[0][q] = twist_in<FU>((double)(int32_t)__builtin_amdgcn_sbfe(tbw[m], 32 - L * P.bgbit, P.bgbit),
+                                               (double)(int32_t)__builtin_amdgcn_sbfe(tbw[m + 8], 32 - L * P.bgbit, P.bgbit),
+                                               twist_t[64 * m]);
+                    }
+                    spin_short_d(tb_read + gi, i + 1, spin_cap, fail);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pair k + 1's pieces landed
+                    counter_add(s_sync + (k1 & 1));
+                    pre_pub = true;
+                    wave_sync();
+                    fft512<1, false, FU, LdsTw, true>(e, Y, T, t);
+                    wave_sync();  // the exchange's reads precede the spectrum's writes
+#pragma unroll
+                    for (int q = 0; q < 8; q++) Y[q * 64 + t] = e[0][q];
+                    __builtin_amdgcn_sched_barrier(0);
+                    counter_add(r5_ready + gi);
+                }
             }
         }
         spin_short_d(fb_ready + gi, (uint32_t)n, spin_cap, fail);  // the last step's b polynomial
@@ -198,7 +231,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     }
 
     // ---- gate wave ----
-    if (tid < 12) s_sync[tid] = 0u;
+    if (tid < 20) s_sync[tid] = 0u;
     for (int x = tid; x < 511; x += 256) s_tw[x] = TT.tw[x];
     for (int x = tid; x < 512; x += 256) s_twist[x] = TT.twist[x];
     int bt = 0;
@@ -263,11 +296,31 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                     for (int m = 0; m < 16; m++)
                         tbx[m] = __builtin_amdgcn_ubfe(tA[m], 32 - L * P.bgbit, P.bgbit) |
                                  (Y32[1024 + t + 64 * m] & ~((1u << P.bgbit) - 1u));
+                    if (VAR == 2) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        counter_add(tb_read + gi);  // Y is the loader's again (this wave's reads came first)
+                    }
                 }
                 pp.mark(5);
-                load_digits_pair_tbx<FU>(d, tbx, rp, P.bgbit, twist_t);
+                if (VAR != 2 || rp != 2) load_digits_pair_tbx<FU>(d, tbx, rp, P.bgbit, twist_t);
             }
-            if (VAR == 1 && rp == 2) {  // knock-out: row 5's transform skipped, its spectrum = row 4's (wrong words)
+            if (VAR == 2 && rp == 2) {  // row 4 here, row 5's spectrum from the loader
+                C2 e[1][8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int m = br3(q);
+                    e[0][q] = twist_in<FU>((double)(int32_t)__builtin_amdgcn_sbfe(tbx[m], 32 - 2 * P.bgbit, P.bgbit),
+                                           (double)(int32_t)__builtin_amdgcn_sbfe(tbx[m + 8], 32 - 2 * P.bgbit, P.bgbit),
+                                           twist_t[64 * m]);
+                }
+                fft512<1, false, FU>(e, X, T, t);
+#pragma unroll
+                for (int q = 0; q < 8; q++) d[0][q] = e[0][q];
+                spin_short_d(r5_ready + gi, (uint32_t)i + 1u, spin_cap, fail);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < 8; q++) d[1][q] = Y[q * 64 + t];
+            } else if (VAR == 1 && rp == 2) {  // knock-out: row 5's transform skipped, its spectrum = row 4's (wrong words)
                 C2 e[1][8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) e[0][q] = d[0][q];
@@ -330,6 +383,11 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 0>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,0> (A/B copy of the assist form)";
+        break;
+    case 2:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 2>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,2> (loader also transforms row 5)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,

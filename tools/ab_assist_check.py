@@ -4,7 +4,7 @@ tools/ab/tfhe_ab_forms.hip) and the oracle: every idle-slot count, the three out
 modes; then timing of one form (BR_FORM=whole|plain|auto).
 Run with TFHE_ALLOW_AB_BUILD=1 TFHE_GPU_LIB=tools/bin/lib_ab.so.
 
-    python tools/ab_assist_check.py parity
+    python tools/ab_assist_check.py parity        (FORM=n checks TFHE_OPT_BR_FORM n instead of the whole form)
     python tools/ab_assist_check.py time STEPS
 """
 import os
@@ -27,6 +27,8 @@ def u32rand(g, *shape):
 
 def parity():
     from oracle import Oracle, params
+    f = os.environ.get("FORM", "whole")
+    form = int(f) if f.isdigit() else f
     o = Oracle()
     p = params("128")
     k0, k1 = o.secret_key(p, 42)
@@ -37,13 +39,13 @@ def parity():
     g = np.random.default_rng(5)
     cts = u32rand(g, 9, p.n + 1)
     want = np.array([o.blind_rotate(p, t, ck.testvec, ck.bk, ck.offset) for t in cts[:3]])
-    with c.options(br_form="whole"):
+    with c.options(br_form=form):
         got = c.blind_rotate_batch(cts[:3])
         print("kernel:", c.last_kernels())
     assert np.array_equal(got, want), "assist TRLWE != oracle"
     with c.options(br_form="plain"):
         ref9 = c.blind_rotate_batch(cts)
-    with c.options(br_form="whole"):
+    with c.options(br_form=form):
         for B in range(1, 10):
             assert np.array_equal(c.blind_rotate_batch(cts[:B]), ref9[:B]), f"idle slots B={B}"
     print("TRLWE outputs bit-exact (oracle on 3, round 4's whole form at B = 1..9)")
@@ -54,7 +56,7 @@ def parity():
     with c.options(br_form="plain"):
         ref = c.gate_batch(ops, A, Bc)
         ref2 = c.bootstrap_without_key_switch_batch(A[:37])
-    with c.options(br_form="whole"):
+    with c.options(br_form=form):
         out = c.gate_batch(ops, A, Bc)
         out2 = c.bootstrap_without_key_switch_batch(A[:37])
     assert np.array_equal(out, ref), f"gate batch: {(out != ref).any(axis=1).sum()} gates differ"
