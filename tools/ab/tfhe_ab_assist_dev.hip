@@ -4,7 +4,9 @@
 // VAR 1 = knock-out timing build: pair 2 runs ONE forward transform (row 4) and reuses it for
 // row 5 (wrong words; the upper bound of moving row 5's transform off the gate wave),
 // VAR 2 = the loader wave also transforms row 5 (b's last level) from its tB words and hands
-// the spectrum to the gate through Y (counters tb_read, r5_ready); same arithmetic and words.
+// the spectrum to the gate through Y (counters tb_read, r5_ready); same arithmetic and words;
+// VAR 3 = VAR 2 with the loader's row-5 exchange 2 in registers, VAR 4 = VAR 2 with the gate's
+// single row-4 transform exchanging through LDS.
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
 namespace tfhe {
@@ -72,6 +74,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
     const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
     constexpr int L = 3;
+    constexpr bool R5 = VAR >= 2;              // the loader transforms row 5
+    constexpr bool R5_EX2LDS = VAR != 3;       // its exchange 2 through LDS (3: in registers)
+    constexpr bool G4_EX2LDS = VAR == 4;       // the gate's single row-4 transform: exchange 2 through LDS
     __shared__ __attribute__((aligned(16))) unsigned char smem[BAD_LDS_TOTAL];
     const int tid = threadIdx.x;
     const int t = tid & 63;
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                 spin_until_ge<LOADER_SLEEP>(s_sync + 2 + (k1 & 1), 4u * (k1 >> 1), loader_cap, fail);
                 issue_bk_pair_async(bkd + (size_t)(k1 / L) * stride + (size_t)(k1 % L) * 2048, s_bk + (k1 & 1) * 2048,
                                     ltid);
-                if (VAR == 2 && k % L == 0) {
+                if (R5 && k % L == 0) {
                     // row 5 (b's last level) of step i: digits from the tB words, forward transform through Y
                     // once the gate has read tB out of it, spectrum handed over in Y (r5_ready); pair k + 1
                     // is published first (its DMA landed under the digits)
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                     counter_add(s_sync + (k1 & 1));
                     pre_pub = true;
                     wave_sync();
-                    fft512<1, false, FU, LdsTw, true>(e, Y, T, t);
+                    fft512<1, false, FU, LdsTw, R5_EX2LDS>(e, Y, T, t);
                     wave_sync();  // the exchange's reads precede the spectrum's writes
 #pragma unroll
                     for (int q = 0; q < 8; q++) Y[q * 64 + t] = e[0][q];
@@ -296,15 +301,15 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                     for (int m = 0; m < 16; m++)
                         tbx[m] = __builtin_amdgcn_ubfe(tA[m], 32 - L * P.bgbit, P.bgbit) |
                                  (Y32[1024 + t + 64 * m] & ~((1u << P.bgbit) - 1u));
-                    if (VAR == 2) {
+                    if (R5) {
                         __builtin_amdgcn_sched_barrier(0);
                         counter_add(tb_read + gi);  // Y is the loader's again (this wave's reads came first)
                     }
                 }
                 pp.mark(5);
-                if (VAR != 2 || rp != 2) load_digits_pair_tbx<FU>(d, tbx, rp, P.bgbit, twist_t);
+                if (!R5 || rp != 2) load_digits_pair_tbx<FU>(d, tbx, rp, P.bgbit, twist_t);
             }
-            if (VAR == 2 && rp == 2) {  // row 4 here, row 5's spectrum from the loader
+            if (R5 && rp == 2) {  // row 4 here, row 5's spectrum from the loader
                 C2 e[1][8];
 #pragma unroll
                 for (int q = 0; q < 8; q++) {
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                                            (double)(int32_t)__builtin_amdgcn_sbfe(tbx[m + 8], 32 - 2 * P.bgbit, P.bgbit),
                                            twist_t[64 * m]);
                 }
-                fft512<1, false, FU>(e, X, T, t);
+                fft512<1, false, FU, LdsTw, G4_EX2LDS>(e, X, T, t);
 #pragma unroll
                 for (int q = 0; q < 8; q++) d[0][q] = e[0][q];
                 spin_short_d(r5_ready + gi, (uint32_t)i + 1u, spin_cap, fail);
@@ -388,6 +393,16 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 2>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,2> (loader also transforms row 5)";
+        break;
+    case 3:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 3>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,3> (row 5 on the loader, its exchange 2 in registers)";
+        break;
+    case 4:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 4>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,4> (row 5 on the loader, gate row 4 exchange 2 in LDS)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
