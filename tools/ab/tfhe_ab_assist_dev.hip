@@ -193,7 +193,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                                                (double)(int32_t)__builtin_amdgcn_sbfe(tbw[m + 8], 32 - L * P.bgbit, P.bgbit),
                                                twist_t[64 * m]);
                     }
+                    lp.mark(6);
                     spin_short_d(tb_read + gi, i + 1, spin_cap, fail);
+                    lp.mark(7);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pair k + 1's pieces landed
                     counter_add(s_sync + (k1 & 1));
                     pre_pub = true;
@@ -204,6 +206,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                     for (int q = 0; q < 8; q++) Y[q * 64 + t] = e[0][q];
                     __builtin_amdgcn_sched_barrier(0);
                     counter_add(r5_ready + gi);
+                    lp.mark(4);
                 }
             }
         }
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
         lp.mark(5);
 #ifdef TFHE_PHASE_PROF
         if (t == 0)
-            for (int q = 0; q < 6; q++) atomicAdd(&g_phase_cycles[8 + q], (unsigned long long)lp.acc[q]);
+            for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[16 + q], (unsigned long long)lp.acc[q]);
 #endif
         report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
         if (FU) near_tie_flag(P, near, g, valid);
@@ -321,7 +324,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                 fft512<1, false, FU, LdsTw, G4_EX2LDS>(e, X, T, t);
 #pragma unroll
                 for (int q = 0; q < 8; q++) d[0][q] = e[0][q];
+                pp.mark(8);
                 spin_short_d(r5_ready + gi, (uint32_t)i + 1u, spin_cap, fail);
+                pp.mark(9);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int q = 0; q < 8; q++) d[1][q] = Y[q * 64 + t];
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     pp.mark(0);
 #ifdef TFHE_PHASE_PROF
     if (t == 0)
-        for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[q], (unsigned long long)pp.acc[q]);
+        for (int q = 0; q < 10; q++) atomicAdd(&g_phase_cycles[q], (unsigned long long)pp.acc[q]);
 #endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU) near_tie_flag(P, near, g, valid);

@@ -6,6 +6,7 @@
 //         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
 #include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
 #include "../zig-tfhe_amd/csrc/tfhe_kernels_whole.hip"
+#include "ab/tfhe_ab_assist_dev.hip"  // "devN": the A/B copy of the assist form, VAR N
 
 #include <cstdio>
 #include <cstdlib>
@@ -53,7 +54,12 @@ int main(int argc, char **argv) {
         const char *form = argc > 2 ? argv[2] : "whole";
         O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
         const bool assist = O.br_form == 1;  // L = 3 fused: the whole form with loader assist
-        CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
+        const bool dev = form[0] == 'd';
+        if (dev)
+            CK(ab_launch_assist_dev(atoi(form + 3), dim3((unsigned)((B + 3) / 4)), dim3(512), 0, P, T, nullptr, d_in,
+                                    nullptr, nullptr, d_tv, (const double2 *)d_bk, d_out, BR_OUT_LV1, B, nullptr));
+        else
+            CK(launch_blind_rotate(P, T, nullptr, d_in, nullptr, nullptr, d_tv, d_bk, d_out, BR_OUT_LV1, B, 0, O));
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
@@ -71,6 +77,20 @@ int main(int argc, char **argv) {
                 for (int w = 0; w < 8; w++) printf(" %8.1f", c[w * 16 + k] / (double)B / P.n);
                 printf("\n");
             }
+            continue;
+        }
+        if (dev) {  // gates [0, 10), loaders [16, 24), per wave-step
+            const char *gn[10] = {"gate: gather+tmp", "gate: pair0 digits+fft", "gate: pub waits", "gate: macs",
+                                  "gate: tB wait+tbx", "gate: pairs1-2 digits+fft", "gate: fb hand-off", "gate: inverse a+store",
+                                  "gate: r5 wait", "gate: r5 spectrum read"};
+            const char *ln[8] = {"loader: vmcnt+pub", "loader: fb wait", "loader: inverse b", "loader: acc_b+gather+tB",
+                                 "loader: refill wait+issue+r5 digits", "loader: tail", "loader: tb_read wait", "loader: row-5 fft+store"};
+            double tot = 0;
+            for (int k = 0; k < 10; k++) tot += c[k];
+            printf("rep %d: %.3f ms (%zu gates, %s); s_memtime ticks per wave-step:\n", rep, ms, B, form);
+            for (int k = 0; k < 10; k++) printf("  %-36s %9.1f  %5.1f%%\n", gn[k], c[k] / (double)B / P.n, 100.0 * c[k] / tot);
+            printf("  %-36s %9.1f\n", "gate total", tot / B / P.n);
+            for (int k = 0; k < 8; k++) printf("  %-36s %9.1f\n", ln[k], c[16 + k] / (double)B / P.n);
             continue;
         }
         if (assist) {  // gates [0, 8), loaders [8, 14), per wave-step
