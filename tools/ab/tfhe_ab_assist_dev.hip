@@ -6,19 +6,23 @@
 // VAR 2 = the loader wave also transforms row 5 (b's last level) from its tB words and hands
 // the spectrum to the gate through Y (counters tb_read, r5_ready); same arithmetic and words;
 // VAR 3 = VAR 2 with the loader's row-5 exchange 2 in registers, VAR 4 = VAR 2 with the gate's
-// single row-4 transform exchanging through LDS.
+// single row-4 transform exchanging through LDS; VAR 5 = VAR 2 with tB handed over as its top 16
+// bits (the gate needs only b's levels 0 and 1) in a 2 KB area of its own, so the loader transforms
+// row 5 through Y at once instead of waiting for the gate to read tB out of Y.
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
 namespace tfhe {
 
 constexpr int BAD_LDS_X = 512 * 16;  // per gate
 constexpr int BAD_LDS_Y = 512 * 16;  // per gate (its loader's)
-constexpr int BAD_LDS_AT = 1024 * 2;
+constexpr int BAD_LDS_AT = 768 * 2;  // a~ of n <= 768 steps (the launcher checks)
 constexpr int BAD_LDS_SYNC = 128;  // pub[2] done[2] fb_ready[4] tb_ready[4] tb_read[4] r5_ready[4]
 constexpr int BAD_X_AT = BR_LDS_BK + BR_LDS_TW + BR_LDS_TWIST;
 constexpr int BAD_Y_AT = BAD_X_AT + BR_WAVES * BAD_LDS_X;
 constexpr int BAD_AT_AT = BAD_Y_AT + BR_WAVES * BAD_LDS_Y;
-constexpr int BAD_LDS_TOTAL = BAD_AT_AT + BR_WAVES * BAD_LDS_AT + BAD_LDS_SYNC;
+constexpr int BAD_LDS_T16 = 1024 * 2;  // VAR 5: tB's top 16 bits per coefficient
+constexpr int BAD_T16_AT = BAD_AT_AT + BR_WAVES * BAD_LDS_AT;
+constexpr int BAD_LDS_TOTAL = BAD_T16_AT + BR_WAVES * BAD_LDS_T16 + BAD_LDS_SYNC;
 static_assert(BAD_LDS_TOTAL <= 160 * 1024, "assist form LDS");
 static_assert(BAD_X_AT % 4096 == 0 && BAD_Y_AT % 4096 == 0 && BAD_LDS_X % 4096 == 0, "gathers need 4 KB-aligned copies");
 
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     constexpr bool R5 = VAR >= 2;              // the loader transforms row 5
     constexpr bool R5_EX2LDS = VAR != 3;       // its exchange 2 through LDS (3: in registers)
     constexpr bool G4_EX2LDS = VAR == 4;       // the gate's single row-4 transform: exchange 2 through LDS
+    constexpr bool T16F = VAR >= 5;            // tB handed over as its top 16 bits in T16 (Y free at once)
     __shared__ __attribute__((aligned(16))) unsigned char smem[BAD_LDS_TOTAL];
     const int tid = threadIdx.x;
     const int t = tid & 63;
@@ -90,6 +95,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     C2 *Y = reinterpret_cast<C2 *>(smem + BAD_Y_AT + gi * BAD_LDS_Y);
     uint32_t *X32 = reinterpret_cast<uint32_t *>(X), *Y32 = reinterpret_cast<uint32_t *>(Y);
     uint16_t *s_at = reinterpret_cast<uint16_t *>(smem + BAD_AT_AT + gi * BAD_LDS_AT);
+    uint16_t *T16 = reinterpret_cast<uint16_t *>(smem + BAD_T16_AT + gi * BAD_LDS_T16);
     uint32_t *s_sync = reinterpret_cast<uint32_t *>(smem + BAD_LDS_TOTAL - BAD_LDS_SYNC);
     uint32_t *fb_ready = s_sync + 4, *tb_ready = s_sync + 8, *tb_read = s_sync + 12, *r5_ready = s_sync + 16;
     if (lds_layout_bad(smem)) {
@@ -168,7 +174,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                 for (int m = 0; m < 16; m++) {
                     const uint32_t sg = gather_sign(xb[m]), off_s = P.offset - sg;
                     tbw[m] = tmp_word(v[m], sg, off_s, accB[m], msbs);
-                    Y32[1024 + t + 64 * m] = tbw[m];
+                    if (T16F)
+                        T16[t + 64 * m] = (uint16_t)(tbw[m] >> 16);
+                    else
+                        Y32[1024 + t + 64 * m] = tbw[m];
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 counter_add(tb_ready + gi);  // tB(i) written (the LDS runs this wave's ops in order)
@@ -194,7 +203,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                                                twist_t[64 * m]);
                     }
                     lp.mark(6);
-                    spin_short_d(tb_read + gi, i + 1, spin_cap, fail);
+                    if (!T16F) spin_short_d(tb_read + gi, i + 1, spin_cap, fail);
                     lp.mark(7);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // pair k + 1's pieces landed
                     counter_add(s_sync + (k1 & 1));
@@ -303,8 +312,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
 #pragma unroll
                     for (int m = 0; m < 16; m++)
                         tbx[m] = __builtin_amdgcn_ubfe(tA[m], 32 - L * P.bgbit, P.bgbit) |
-                                 (Y32[1024 + t + 64 * m] & ~((1u << P.bgbit) - 1u));
-                    if (R5) {
+                                 (T16F ? (uint32_t)T16[t + 64 * m] << 16 : (Y32[1024 + t + 64 * m] & ~((1u << P.bgbit) - 1u)));
+                    if (R5 && !T16F) {
                         __builtin_amdgcn_sched_barrier(0);
                         counter_add(tb_read + gi);  // Y is the loader's again (this wave's reads came first)
                     }
@@ -388,6 +397,7 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
                                 const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                 const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B,
                                 const char **used) {
+    if (P.n > BAD_LDS_AT / 2) return hipErrorInvalidValue;
     switch (var) {
     case 0:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 0>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
@@ -408,6 +418,11 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 4>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,4> (row 5 on the loader, gate row 4 exchange 2 in LDS)";
+        break;
+    case 5:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 5>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,5> (row 5 on the loader, tB's top half in its own LDS area)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
