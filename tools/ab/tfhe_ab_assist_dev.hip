@@ -8,7 +8,8 @@
 // VAR 3 = VAR 2 with the loader's row-5 exchange 2 in registers, VAR 4 = VAR 2 with the gate's
 // single row-4 transform exchanging through LDS; VAR 5 = VAR 2 with tB handed over as its top 16
 // bits (the gate needs only b's levels 0 and 1) in a 2 KB area of its own, so the loader transforms
-// row 5 through Y at once instead of waiting for the gate to read tB out of Y.
+// row 5 through Y at once instead of waiting for the gate to read tB out of Y; VAR 6 = VAR 0 with
+// the gate's pipelined forward pairs exchanging stage 2 in registers (fewer LDS operations).
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
 namespace tfhe {
@@ -70,6 +71,30 @@ DEV void spin_short_d(const uint32_t *p, uint32_t target, uint32_t cap, uint32_t
     uint32_t f = 0;
     spin_until_ge<1>(p, target, cap, f);
     fail |= f;
+}
+
+// The pipelined transform pair of fft512_x2 (tfhe_device.hpp, one buffer) with exchange 2 in
+// registers (ex2_regs: permlane swaps + DPP) instead of LDS: 16 ds_write/read_b128 fewer per
+// transform for 80 VALU moves each.  Same values (pure data movement).
+template <bool INV, bool FU, class TW>
+DEV void fft512_x2_ex2r(C2 (*d)[8], C2 *xb, const TW &T, int t) {
+    C2 wb_[7], wc_[7];
+    passA<INV, FU>(d[0], T.a);
+    ex1_write(d[0], xb, t);
+    wave_sync();
+    passA<INV, FU>(d[1], T.a);
+    ex1_read(d[0], xb, t);
+    ex1_write(d[1], xb, t);
+    wave_sync();
+    T.pass_b(wb_, t);
+    passBC<INV, FU>(d[0], wb_);
+    ex1_read(d[1], xb, t);
+    ex2_regs(d[0]);
+    passBC<INV, FU>(d[1], wb_);
+    T.pass_c(wc_, t);
+    ex2_regs(d[1]);
+    passBC<INV, FU>(d[0], wc_);
+    passBC<INV, FU>(d[1], wc_);
 }
 
 template <bool FU, int VAR>
@@ -347,7 +372,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
 #pragma unroll
                 for (int q = 0; q < 8; q++) d[0][q] = d[1][q] = e[0][q];
             } else {
-                fft512_x2<false, true, FU>(d, X, T, t);
+                if (VAR == 6)
+                    fft512_x2_ex2r<false, FU>(d, X, T, t);
+                else
+                    fft512_x2<false, true, FU>(d, X, T, t);
             }
             const uint32_t k = (uint32_t)(L * i + rp);
             pp.mark(2);
@@ -423,6 +451,11 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 5>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,5> (row 5 on the loader, tB's top half in its own LDS area)";
+        break;
+    case 6:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 6>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,6> (forward pairs: exchange 2 in registers)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,

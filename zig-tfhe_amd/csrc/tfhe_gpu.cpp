@@ -1786,7 +1786,7 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     case TFHE_OPT_BR_FORM:
         // 2 split, 4 pair: removed in round 4; 6 duo, 7 split-transform latency
         // form, 8 the whole form without loader assist: A/B libraries only (tools/ab/); 5 octo: L = 1 only
-        ok = v == 0 || v == 1 || v == 3 || (v == 5 && c->P.L == 1) || (v >= 6 && v <= 15 && ab_forms_linked());
+        ok = v == 0 || v == 1 || v == 3 || (v == 5 && c->P.L == 1) || (v >= 6 && v <= 40 && ab_forms_linked());
         if (!ok && v == 5) why = "TFHE_OPT_BR_FORM 5 (octo form) exists at L = 1 only";
         if (!ok && v >= 6 && v <= 8) why = "TFHE_OPT_BR_FORM " + std::to_string(v) + ": an A/B-only form, not in the product library (tools/ab/)";
         break;
