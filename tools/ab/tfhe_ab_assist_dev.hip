@@ -9,7 +9,8 @@
 // single row-4 transform exchanging through LDS; VAR 5 = VAR 2 with tB handed over as its top 16
 // bits (the gate needs only b's levels 0 and 1) in a 2 KB area of its own, so the loader transforms
 // row 5 through Y at once instead of waiting for the gate to read tB out of Y; VAR 6 = VAR 0 with
-// the gate's pipelined forward pairs exchanging stage 2 in registers (fewer LDS operations).
+// the gate's pipelined forward pairs exchanging stage 2 in registers (fewer LDS operations);
+// VAR 7 / 8 / 9: the same for pair 0 / pair 2 / pairs 1-2 only.
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
 namespace tfhe {
@@ -372,7 +373,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
 #pragma unroll
                 for (int q = 0; q < 8; q++) d[0][q] = d[1][q] = e[0][q];
             } else {
-                if (VAR == 6)
+                if (VAR == 6 || (VAR == 7 && rp == 0) || (VAR == 8 && rp == 2) || (VAR == 9 && rp > 0))
                     fft512_x2_ex2r<false, FU>(d, X, T, t);
                 else
                     fft512_x2<false, true, FU>(d, X, T, t);
@@ -456,6 +457,21 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 6>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,6> (forward pairs: exchange 2 in registers)";
+        break;
+    case 7:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 7>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,7> (exchange 2 in registers: pair 0)";
+        break;
+    case 8:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 8>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,8> (exchange 2 in registers: pair 2)";
+        break;
+    case 9:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 9>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,9> (exchange 2 in registers: pairs 1-2)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
