@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 6  /* 6: tfhe_gpu_build_kind, tfhe_lut_generate_scaled / _full; BR forms 6/7
+#define TFHE_GPU_ABI_VERSION 6  /* 6: tfhe_gpu_build_kind, tfhe_lut_generate_scaled / _full; BR forms 6-40
                                    A/B-only, BR_LOADER / BR_SYNC = 1 only;
                                    5: _dev LUT / re-encryption / circuit entries; BR forms 2 and 4 removed */
 
@@ -154,9 +154,10 @@ int tfhe_gpu_near_tie_items(const tfhe_gpu_ctx *ctx, uint64_t *count);
 enum {
     TFHE_OPT_BR_FORM = 1,         /* blind rotation: 0 auto (default), 1 whole, 3 latency, 5 octo (8 items
                                      per workgroup, two gate waves per SIMD; L = 1 only).  2 split and 4
-                                     pair were removed in round 4; 6 duo and 7 the split-transform latency
-                                     form (both measured slower) exist only in A/B
-                                     libraries since round 5 (tools/ab/): TFHE_ERR_INVALID here */
+                                     pair were removed in round 4; 6 duo, 7 the split-transform latency
+                                     form, 8 round 4's whole form and 9-40 development copies of the L = 3
+                                     whole form (all measured slower) exist
+                                     only in A/B libraries since round 5 (tools/ab/): TFHE_ERR_INVALID here */
     TFHE_OPT_BR_LOADER = 2,       /* whole form: 1 loader waves issue the BK DMAs (the only value since
                                      round 5; 0, the gate waves issuing them, was removed) */
     TFHE_OPT_KS_FORM = 3,         /* key switch: 3 auto (default: the one-hot GEMM on the matrix
