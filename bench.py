@@ -292,7 +292,7 @@ def timed_circuit(ctx, circ, inputs, args, world, device):
     ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
     el, _ = timed(lambda: circ.run_dev(ctx, t_in.data_ptr(), t_out.data_ptr()), args.steps, args.warmup, world, device)
     outs = t_out.cpu().numpy().view(np.uint32)
-    ctx.set_stream(0)
+    ctx.set_stream(None)
     return el, outs, depth, el_host, outs_host
 
 
@@ -418,7 +418,7 @@ def run_workload(args, rank, world, device):
         el, _ = timed(lambda: hr.reencrypt_dev(t_in.data_ptr(), t_out.data_ptr(), B), args.steps, args.warmup,
                       world, device)
         outs = t_out.cpu().numpy().view(np.uint32)
-        ctx.set_stream(0)
+        ctx.set_stream(None)
         ok = bool(np.array_equal(bob.decrypt_bool(outs), bits.astype(bool))) and bool(np.array_equal(outs, outs_host))
         hr.close()
         units = total * args.steps
@@ -444,7 +444,7 @@ def run_workload(args, rank, world, device):
         el, _ = timed(lambda: ctx.bootstrap_lut_batch_dev(t_in.data_ptr(), t_tv.data_ptr(), t_out.data_ptr(), B),
                       args.steps, args.warmup, world, device)
         outs = t_out.cpu().numpy().view(np.uint32)
-        ctx.set_stream(0)
+        ctx.set_stream(None)
         ok = bool(np.array_equal(sk.decrypt_lwe_message(outs, m), (msgs * msgs + 3) % m)) and \
             bool(np.array_equal(outs, outs_host))
         units = total * args.steps

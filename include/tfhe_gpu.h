@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define TFHE_GPU_ABI_VERSION 6  /* 6: tfhe_gpu_build_kind, tfhe_lut_generate_scaled / _full; BR forms 6-40
+#define TFHE_GPU_ABI_VERSION 7  /* 7: tfhe_gpu_set_stream(NULL) = the null stream, tfhe_gpu_reset_stream;
+                                   6: tfhe_gpu_build_kind, tfhe_lut_generate_scaled / _full; BR forms 6-40
                                    A/B-only, BR_LOADER / BR_SYNC = 1 only;
                                    5: _dev LUT / re-encryption / circuit entries; BR forms 2 and 4 removed */
 
@@ -101,9 +102,14 @@ const char *tfhe_gpu_last_error(const tfhe_gpu_ctx *ctx);
  * performs the same check before it returns; after the asynchronous _dev
  * entry points, this (or tfhe_gpu_profile_end) is where a failure surfaces. */
 int         tfhe_gpu_sync(tfhe_gpu_ctx *ctx);
-/* Run this context's work on a caller-owned hipStream_t (NULL = own stream).
- * Multi-device context: the stream of its first device. */
+/* Run this context's work on a caller-owned hipStream_t of its device; NULL is
+ * that device's null stream (torch's default stream has handle 0).  The new
+ * stream first waits for everything queued on the old one.  (ABI 7: before,
+ * NULL meant the context's own stream, so torch's default stream silently got
+ * an unordered non-blocking stream.)  Multi-device context: its first device. */
 int         tfhe_gpu_set_stream(tfhe_gpu_ctx *ctx, void *hip_stream);
+/* Back to the context's own (non-blocking) stream, ordered after the current one.  (ABI 7) */
+int         tfhe_gpu_reset_stream(tfhe_gpu_ctx *ctx);
 
 /* ---- Multi-device context (bootstrap.zig:30-47 strategy over
  * the 8 GPUs of one node) ---------------------------------------------------

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 6
+    assert tfhe_amd.load_library().tfhe_gpu_abi_version() == 7
 
 
 def test_library_is_not_an_ab_build():

@@ -133,7 +133,7 @@ def test_circuit_device_resident(oracle, shape):
         d2 = c.run_dev(ctx, t_in.data_ptr(), t_out.data_ptr())
         ctx.sync()
     finally:
-        ctx.set_stream(0)
+        ctx.set_stream(None)
     assert d2 == depth
     assert np.array_equal(t_out.cpu().numpy().view(np.uint32), want)
     if shape == "adder128":

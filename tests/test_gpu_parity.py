@@ -344,7 +344,7 @@ def test_lut_device_resident(oracle, pname, B):
         c.bootstrap_lut_batch_dev(t_in.data_ptr(), t_tv.data_ptr(), t_out.data_ptr(), B)
         c.sync()
     finally:
-        c.set_stream(0)
+        c.set_stream(None)
     got = t_out.cpu().numpy().view(np.uint32)
     assert np.array_equal(got, want)
     one = oracle.gate_batch(k.p, np.array([255], np.uint8), cts[B - 1][None], cts[B - 1][None], k.ck, testvec=tv)[0]
@@ -525,6 +525,39 @@ def test_device_resident_api_with_torch(oracle):
     finally:
         c.set_stream(None)
     assert np.array_equal(t_o.cpu().numpy().view(np.uint32), want)
+
+
+def test_dev_entry_ordered_on_torch_default_stream(oracle):
+    """ABI 7: torch's default stream has handle 0, the device's null stream, and
+    tfhe_gpu_set_stream(ctx, NULL) now means that stream (up to ABI 6 it meant the
+    context's own non-blocking stream, so a torch op right after a _dev call could
+    read the outputs before they were written: tools/soak_fused.py found it).  A
+    4,096-gate batch (tens of ms) followed by a torch copy on the same stream, with
+    no device-wide synchronisation in between: the copy sees every output word."""
+    torch = pytest.importorskip("torch")
+    c, k = ctx_for(oracle, "128")
+    g = rng(12)
+    B = 4096
+    ops = (np.arange(B) % 10).astype(np.uint8)
+    A, Bc = u32rand(g, B, k.p.n + 1), u32rand(g, B, k.p.n + 1)
+    want = c.gate_batch(ops, A, Bc)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    assert stream.cuda_stream == 0  # the default stream: the case that used to race
+    t_ops = torch.from_numpy(ops).to(dev)
+    t_a = torch.from_numpy(A.view(np.int32)).to(dev)
+    t_b = torch.from_numpy(Bc.view(np.int32)).to(dev)
+    t_o = torch.zeros_like(t_a)
+    torch.cuda.synchronize(dev)
+    c.set_stream(stream.cuda_stream)
+    try:
+        c.gate_batch_dev(t_ops.data_ptr(), t_a.data_ptr(), t_b.data_ptr(), t_o.data_ptr(), B)
+        snap = t_o.clone()  # queued on torch's stream right behind the library's launches
+        got = snap.cpu().numpy().view(np.uint32)
+    finally:
+        c.set_stream(None)
+    c.sync()
+    assert np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("gw", [0, 1, 2, 4, 8])

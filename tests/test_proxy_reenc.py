@@ -236,7 +236,7 @@ def test_gpu_reencrypt_device_resident(oracle, P, keys, reenc_ab, ks_form):
                 assert np.array_equal(got, want), B
                 assert np.array_equal(got[B - 1], oracle.reencrypt(P.n, P.basebit, P.iks_t, x[B - 1], reenc_ab))
     finally:
-        ctx.set_stream(0)
+        ctx.set_stream(None)
         hr.close()
         ctx.close()
 

@@ -93,7 +93,7 @@ def timing(steps):
     ok = np.array_equal(sk.decrypt_bool(t_o.cpu().numpy().view(np.uint32)), ~(a.astype(bool) & b.astype(bool)))
     print(f"{form} ({tfhe_amd.build_id()}): {el / steps * 1e3:.3f} ms per 1,024 NAND, {1024 * steps / el:.0f}/s, "
           f"decrypt {ok}, {c.last_kernels()}")
-    c.set_stream(0)
+    c.set_stream(None)
     c.close()
 
 

@@ -602,7 +602,7 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     if (!c) return;
     destroy_shards(c);
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->stream);  // NULL is a valid stream here (the device's null stream)
     for (void *p : {(void *)c->d_err, (void *)c->d_twist, (void *)c->d_tw, (void *)c->d_testvec, (void *)c->d_bk, (void *)c->d_ksk,
                     c->s_a.p, c->s_b.p, c->s_out.p, c->s_lv1.p, c->s_ops.p, c->s_tv.p, c->s_tmp.p, c->s_ties.p,
                     c->s_wires.p, c->s_cidx.p, c->s_cops.p, c->s_kspart.p, (void *)c->d_ksk_gemm})
@@ -645,9 +645,7 @@ int tfhe_gpu_sync(tfhe_gpu_ctx *c) {
 // The context queues its own work on its stream too (the MFMA-layout KSK build,
 // the near-tie flag and error-word clears): the new stream waits for everything
 // queued on the old one, so a _dev call on the new stream never overtakes it.
-int tfhe_gpu_set_stream(tfhe_gpu_ctx *c, void *s) {
-    if (!c) return TFHE_ERR_INVALID;
-    hipStream_t ns = s ? (hipStream_t)s : c->own_stream;
+static int switch_stream(tfhe_gpu_ctx *c, hipStream_t ns) {
     if (ns == c->stream) return TFHE_OK;
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->stream_ev) HIPCHK(c, hipEventCreateWithFlags(&c->stream_ev, hipEventDisableTiming));
@@ -655,6 +653,20 @@ int tfhe_gpu_set_stream(tfhe_gpu_ctx *c, void *s) {
     HIPCHK(c, hipStreamWaitEvent(ns, c->stream_ev, 0));
     c->stream = ns;
     return TFHE_OK;
+}
+
+// ABI 7: NULL is the device's null stream (torch's default stream has handle 0),
+// no longer "back to the context's own stream", which is tfhe_gpu_reset_stream.
+// Up to ABI 6 a caller passing torch's default stream got the context's own
+// non-blocking stream, unordered with torch's work.
+int tfhe_gpu_set_stream(tfhe_gpu_ctx *c, void *s) {
+    if (!c) return TFHE_ERR_INVALID;
+    return switch_stream(c, (hipStream_t)s);
+}
+
+int tfhe_gpu_reset_stream(tfhe_gpu_ctx *c) {
+    if (!c) return TFHE_ERR_INVALID;
+    return switch_stream(c, c->own_stream);
 }
 
 int tfhe_gpu_load_cloud_key(tfhe_gpu_ctx *c, uint32_t offset, const uint32_t *tv_a, const uint32_t *tv_b,

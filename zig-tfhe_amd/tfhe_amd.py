@@ -92,6 +92,7 @@ _SIGS = {
     "tfhe_gpu_last_error": (C.c_char_p, [vp]),
     "tfhe_gpu_sync": (C.c_int, [vp]),
     "tfhe_gpu_set_stream": (C.c_int, [vp, vp]),
+    "tfhe_gpu_reset_stream": (C.c_int, [vp]),
     "tfhe_gpu_create_multi": (C.c_int, [C.POINTER(TfheParams), C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
     "tfhe_gpu_num_devices": (C.c_int, [vp]),
     "tfhe_gpu_device_bootstraps": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_int]),
@@ -395,7 +396,12 @@ class Context:
                    "import_key_device")
 
     def set_stream(self, stream_ptr: int | None):
-        self.check(self.lib.tfhe_gpu_set_stream(self.h, vp(stream_ptr or 0)), "set_stream")
+        """Run on a HIP stream handle (e.g. torch.cuda.current_stream().cuda_stream; 0 is the
+        device's null stream, torch's default stream); None: back to the context's own stream."""
+        if stream_ptr is None:
+            self.check(self.lib.tfhe_gpu_reset_stream(self.h), "reset_stream")
+        else:
+            self.check(self.lib.tfhe_gpu_set_stream(self.h, vp(stream_ptr)), "set_stream")
 
     def sync(self):
         self.check(self.lib.tfhe_gpu_sync(self.h), "sync")
