@@ -10,7 +10,8 @@
 // bits (the gate needs only b's levels 0 and 1) in a 2 KB area of its own, so the loader transforms
 // row 5 through Y at once instead of waiting for the gate to read tB out of Y; VAR 6 = VAR 0 with
 // the gate's pipelined forward pairs exchanging stage 2 in registers (fewer LDS operations);
-// VAR 7 / 8 / 9: the same for pair 0 / pair 2 / pairs 1-2 only.
+// VAR 7 / 8 / 9: the same for pair 0 / pair 2 / pairs 1-2 only; VAR 10 = knock-out timing build:
+// the forward pairs skip exchange 2 altogether (wrong words; what half the exchange traffic is worth).
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
 namespace tfhe {
@@ -94,6 +95,26 @@ DEV void fft512_x2_ex2r(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     passBC<INV, FU>(d[1], wb_);
     T.pass_c(wc_, t);
     ex2_regs(d[1]);
+    passBC<INV, FU>(d[0], wc_);
+    passBC<INV, FU>(d[1], wc_);
+}
+
+// Knock-out (VAR 10, timing only, wrong words): the pair with exchange 2 skipped entirely.
+template <bool INV, bool FU, class TW>
+DEV void fft512_x2_noex2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
+    C2 wb_[7], wc_[7];
+    passA<INV, FU>(d[0], T.a);
+    ex1_write(d[0], xb, t);
+    wave_sync();
+    passA<INV, FU>(d[1], T.a);
+    ex1_read(d[0], xb, t);
+    ex1_write(d[1], xb, t);
+    wave_sync();
+    T.pass_b(wb_, t);
+    passBC<INV, FU>(d[0], wb_);
+    ex1_read(d[1], xb, t);
+    passBC<INV, FU>(d[1], wb_);
+    T.pass_c(wc_, t);
     passBC<INV, FU>(d[0], wc_);
     passBC<INV, FU>(d[1], wc_);
 }
@@ -375,6 +396,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
             } else {
                 if (VAR == 6 || (VAR == 7 && rp == 0) || (VAR == 8 && rp == 2) || (VAR == 9 && rp > 0))
                     fft512_x2_ex2r<false, FU>(d, X, T, t);
+                else if (VAR == 10)
+                    fft512_x2_noex2<false, FU>(d, X, T, t);
                 else
                     fft512_x2<false, true, FU>(d, X, T, t);
             }
@@ -472,6 +495,11 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 9>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,9> (exchange 2 in registers: pairs 1-2)";
+        break;
+    case 10:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 10>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,10> (knock-out: forward exchange 2 skipped, wrong words)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
