@@ -279,7 +279,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
             for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[16 + q], (unsigned long long)lp.acc[q]);
 #endif
         report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
-        if (FU) near_tie_flag(P, near, g, valid);
+        if (FU && VAR != 10) near_tie_flag(P, near, g, valid);  // VAR 10: garbage values, no recompute
         if (!valid) return;
         // the b parts of the outputs (accB: coefficient t + 64m)
         if (out_mode == BR_OUT_LV1) {
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
         for (int q = 0; q < 10; q++) atomicAdd(&g_phase_cycles[q], (unsigned long long)pp.acc[q]);
 #endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
-    if (FU) near_tie_flag(P, near, g, valid);
+    if (FU && VAR != 10) near_tie_flag(P, near, g, valid);  // VAR 10: garbage values, no recompute
     if (!valid) return;
     // the a parts of the outputs from the acc_a copy (the loader writes b's)
     if (out_mode == BR_OUT_LV1) {  // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j]; p[N] = b[0]: loader
