@@ -222,6 +222,18 @@ def rooflines(p, B, params, br_avg_s, kernel):
         f64_insts = pmc.get("valu_f64_insts_per_launch", 0) + pmc.get("valu_fma_f64_insts_per_launch", 0)
         if f64_insts:
             roof["pmc"]["valu_f64_frac_from_pmc"] = round(f64_insts * 64 / br_avg_s / VALU_F64_PEAK, 4)
+        # what binds the step: the SIMD's VALU issue for the item as a whole (gate
+        # and loader waves, f64 and integer), measured as wave-instructions per SIMD per launch
+        # (PMC SQ_INSTS_VALU / 1,024 SIMDs) against the sustained issue interval of tools/isa_rate.hip
+        # (2.01 ns per wave-instruction per SIMD for v_add/v_mul_f64 at 4 waves per SIMD; 2.14 ns at 2)
+        insts = pmc.get("raw_per_launch", {}).get("SQ_INSTS_VALU")
+        if insts:
+            ns = br_avg_s * 1e9 / (insts / (256 * 4))
+            roof["valu_issue"] = {"ns_per_valu_inst_per_simd": round(ns, 3), "peak_ns_4_waves": 2.01,
+                                  "peak_ns_2_waves": 2.14, "frac": round(2.01 / ns, 4),
+                                  "valu_insts_per_item_per_cmux": pmc.get("valu_insts_per_item_per_cmux"),
+                                  "note": "issue interval achieved vs the measured sustained f64 VALU interval; "
+                                          "the kernel runs 2 waves per SIMD (gate + loader)"}
         # the DRAM side of the same kernel: measured bytes per launch / kernel time / HBM peak
         roof["dram"] = {"achieved_gbs": round(pmc["hbm_bytes_per_launch"] / br_avg_s / 1e9, 1),
                         "peak_gbs": HBM_PEAK_BPS / 1e9,
