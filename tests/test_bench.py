@@ -1,0 +1,64 @@
+"""The bench line's host-side arithmetic (bench.py), on CPU: the f64 operation
+model behind roofline.achieved, the rank split of weak and strong scaling, and
+the roofline object built from the committed PMC and rocprof records (the same
+numbers the GPU line reports, recomputed here from the files)."""
+import csv
+import json
+import os
+import types
+
+import pytest
+
+import bench
+import tfhe_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_f64_model():
+    # 145,424 fused / 243,760 reference-tree f64 lane-ops per CMUX at L = 3
+    assert bench.f64_ops_per_cmux(3, True) == 145424
+    assert bench.f64_ops_per_cmux(3) == 243760
+    # 8 transforms x (511 j=0 butterflies x 4 + 1,793 twiddled x 6), 6 twists + 2 untwists x 512 x 4,
+    # 6 rows x 2 outputs x 512 MAC terms x 4, 2,048 one-add conversions
+    fft = 511 * 4 + 1793 * 6
+    assert 8 * fft + 8 * 2048 + 12 * 2048 + 2048 == 145424
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_rank_split(world):
+    weak = types.SimpleNamespace(global_batch=0, batch=1024)
+    strong = types.SimpleNamespace(global_batch=65536 + 5, batch=1024)
+    assert [bench.per_rank_batch(weak, r, world) for r in range(world)] == [(1024, 1024 * world, "weak")] * world
+    parts = [bench.per_rank_batch(strong, r, world) for r in range(world)]
+    assert sum(p[0] for p in parts) == 65541 and max(p[0] for p in parts) - min(p[0] for p in parts) <= 1
+    assert all(p[1:] == (65541, "strong") for p in parts)
+
+
+def test_roofline_from_committed_records(monkeypatch):
+    """roofline.frac_rocprof and roofline.valu_issue from profiles/ reproduce by hand
+    from the committed csv and PMC file, for the build id those records carry."""
+    pmc = json.load(open(bench.PMC_PATH))
+    rp = json.load(open(bench.ROCPROF_PATH))
+    assert pmc["kernel_build_id"] == rp["kernel_build_id"]
+    monkeypatch.setattr(bench, "kernel_build_id", lambda: pmc["kernel_build_id"])  # the records' binary
+    p = tfhe_amd.make_params("128")
+    kernel_s = 5.97e-3
+    roof, key = bench.rooflines(p, 1024, "128", kernel_s, "k_blind_rotate_assist<true> (whole form, fused)")
+    ops = 145424 * 700 * 1024
+    assert roof["algorithmic_f64_ops_per_launch"] == ops
+    assert roof["frac"] == pytest.approx(ops / kernel_s / bench.VALU_F64_PEAK, abs=1e-4)
+    # rocprof basis: (TotalDurationNs - MaxNs) / (Calls - 1) of the csv row named in the record
+    src = os.path.join(ROOT, rp["source"])
+    row = next(r for r in csv.DictReader(open(src)) if r["Name"].startswith(rp["kernel"] + "("))
+    avg_ms = (float(row["TotalDurationNs"]) - float(row["MaxNs"])) / (int(row["Calls"]) - 1) / 1e6
+    assert roof["kernel_avg_ms_rocprof"] == pytest.approx(avg_ms, abs=1e-3)
+    assert roof["frac_rocprof"] == pytest.approx(ops / (avg_ms / 1e3) / bench.VALU_F64_PEAK, abs=1e-4)
+    # VALU issue: wave-instructions per SIMD per launch against the kernel time
+    ns = kernel_s * 1e9 / (pmc["raw_per_launch"]["SQ_INSTS_VALU"] / 1024)
+    assert roof["valu_issue"]["ns_per_valu_inst_per_simd"] == pytest.approx(ns, abs=1e-3)
+    assert roof["valu_issue"]["frac"] == pytest.approx(2.01 / ns, abs=1e-4)
+    # DRAM side: measured bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, KB x1024)
+    raw = pmc["raw_per_launch"]
+    assert roof["traffic"] == int(raw["FETCH_SIZE"] * 1024 * 2 + raw["WRITE_SIZE"] * 1024)
+    assert key["key_bytes_consumed_per_launch"] == bench.algorithmic_bytes_per_gate(p) * 1024
