@@ -11,7 +11,10 @@
 // row 5 through Y at once instead of waiting for the gate to read tB out of Y; VAR 6 = VAR 0 with
 // the gate's pipelined forward pairs exchanging stage 2 in registers (fewer LDS operations);
 // VAR 7 / 8 / 9: the same for pair 0 / pair 2 / pairs 1-2 only; VAR 10 = knock-out timing build:
-// the forward pairs skip exchange 2 altogether (wrong words; what half the exchange traffic is worth).
+// the forward pairs skip exchange 2 altogether (wrong words; what half the exchange traffic is worth);
+// VAR 11 = VAR 0 with the slot counter and the MAC's first BK group read under the pair's last pass;
+// VAR 12 = VAR 5 with pair 1's exchange 2 in registers.  (Until this fix VAR 6-10 also carried
+// VAR 5's row-5 split: R5 was VAR >= 2; profiles/r05_ab_ex2_regs.txt records both.)
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
 namespace tfhe {
@@ -99,6 +102,46 @@ DEV void fft512_x2_ex2r(C2 (*d)[8], C2 *xb, const TW &T, int t) {
     passBC<INV, FU>(d[1], wc_);
 }
 
+// VAR 13: fft512_x2 (one buffer) with the MAC's slot counter and first BK frequency group read
+// EARLY, right behind transform 1's exchange-2 reads and before its last pass, so their LDS
+// latency runs under that pass instead of in front of the MAC.  The wave's LDS operations
+// execute in order, so BK words read behind a counter value that says "published" are the
+// published ones; a counter that does not yet say so sends the caller to the usual wait.
+template <bool INV, bool FU, class TW>
+DEV void fft512_x2_early(C2 (*d)[8], C2 *xb, const TW &T, int t, const uint32_t *pubp, const double2 *slot_t,
+                         uint32_t &cnt, double2 *kpre) {
+    C2 wb_[7], wc_[7];
+    passA<INV, FU>(d[0], T.a);
+    ex1_write(d[0], xb, t);
+    wave_sync();
+    passA<INV, FU>(d[1], T.a);
+    ex1_read(d[0], xb, t);
+    ex1_write(d[1], xb, t);
+    wave_sync();
+    T.pass_b(wb_, t);
+    passBC<INV, FU>(d[0], wb_);
+    ex1_read(d[1], xb, t);
+    ex2_write(d[0], xb, t);
+    wave_sync();
+    passBC<INV, FU>(d[1], wb_);
+    T.pass_c(wc_, t);
+    ex2_read(d[0], xb, t);
+    ex2_write(d[1], xb, t);
+    wave_sync();
+    passBC<INV, FU>(d[0], wc_);
+    ex2_read(d[1], xb, t);
+    wave_sync();
+    cnt = *(volatile const uint32_t *)pubp;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_sched_barrier(0);
+    kpre[0] = slot_t[0];
+    kpre[1] = slot_t[64];
+    kpre[2] = slot_t[1024];
+    kpre[3] = slot_t[1088];
+    __builtin_amdgcn_sched_barrier(0);
+    passBC<INV, FU>(d[1], wc_);
+}
+
 // Knock-out (VAR 10, timing only, wrong words): the pair with exchange 2 skipped entirely.
 template <bool INV, bool FU, class TW>
 DEV void fft512_x2_noex2(C2 (*d)[8], C2 *xb, const TW &T, int t) {
@@ -125,10 +168,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
     const double2 *__restrict__ bkd, uint32_t *__restrict__ out, int out_mode, size_t B) {
     constexpr int L = 3;
-    constexpr bool R5 = VAR >= 2;              // the loader transforms row 5
+    constexpr bool R5 = (VAR >= 2 && VAR <= 5) || VAR == 12;  // the loader transforms row 5
     constexpr bool R5_EX2LDS = VAR != 3;       // its exchange 2 through LDS (3: in registers)
     constexpr bool G4_EX2LDS = VAR == 4;       // the gate's single row-4 transform: exchange 2 through LDS
-    constexpr bool T16F = VAR >= 5;            // tB handed over as its top 16 bits in T16 (Y free at once)
+    constexpr bool T16F = VAR == 5 || VAR == 12;  // tB handed over as its top 16 bits in T16 (Y free at once)
     __shared__ __attribute__((aligned(16))) unsigned char smem[BAD_LDS_TOTAL];
     const int tid = threadIdx.x;
     const int t = tid & 63;
@@ -394,16 +437,23 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
 #pragma unroll
                 for (int q = 0; q < 8; q++) d[0][q] = d[1][q] = e[0][q];
             } else {
-                if (VAR == 6 || (VAR == 7 && rp == 0) || (VAR == 8 && rp == 2) || (VAR == 9 && rp > 0))
+                if (VAR == 6 || (VAR == 7 && rp == 0) || (VAR == 8 && rp == 2) || (VAR == 9 && rp > 0) ||
+                    (VAR == 12 && rp == 1))
                     fft512_x2_ex2r<false, FU>(d, X, T, t);
                 else if (VAR == 10)
                     fft512_x2_noex2<false, FU>(d, X, T, t);
-                else
+                else if (VAR != 11)
                     fft512_x2<false, true, FU>(d, X, T, t);
             }
             const uint32_t k = (uint32_t)(L * i + rp);
+            bool early_ok = false;
+            if (VAR == 11 && !(R5 && rp == 2)) {
+                uint32_t cnt;
+                fft512_x2_early<false, FU>(d, X, T, t, s_sync + (k & 1), s_bk + (k & 1) * 2048 + t, cnt, kpre);
+                early_ok = __builtin_amdgcn_readfirstlane(cnt) >= 4u * ((k >> 1) + 1u);
+            }
             pp.mark(2);
-            wait_pair_first_group(s_sync, s_bk + (k & 1) * 2048 + t, k, spin_cap, fail, kpre);
+            if (!early_ok) wait_pair_first_group(s_sync, s_bk + (k & 1) * 2048 + t, k, spin_cap, fail, kpre);
             __builtin_amdgcn_sched_barrier(0);
             pp.mark(3);
             mac_pair_lds<FU>(fa, fb, d[0], d[1], s_bk + (k & 1) * 2048, t, kpre);
@@ -500,6 +550,16 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 10>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,10> (knock-out: forward exchange 2 skipped, wrong words)";
+        break;
+    case 11:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 11>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,11> (slot counter + first BK group read under the last pass)";
+        break;
+    case 12:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 12>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,12> (row 5 on the loader as VAR 5, pair 1 exchange 2 in registers)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
