@@ -13,7 +13,9 @@
 // VAR 7 / 8 / 9: the same for pair 0 / pair 2 / pairs 1-2 only; VAR 10 = knock-out timing build:
 // the forward pairs skip exchange 2 altogether (wrong words; what half the exchange traffic is worth);
 // VAR 11 = VAR 0 with the slot counter and the MAC's first BK group read under the pair's last pass;
-// VAR 12 = VAR 5 with pair 1's exchange 2 in registers.  (Until this fix VAR 6-10 also carried
+// VAR 12 = VAR 5 with pair 1's exchange 2 in registers; VAR 13 = VAR 0 with each forward pair's
+// transform 0 exchanging stage 2 in registers and transform 1 through LDS; VAR 14 = knock-out
+// timing build: VAR 13 with transform 0's exchange 2 skipped (wrong words).  (Until this fix VAR 6-10 also carried
 // VAR 5's row-5 split: R5 was VAR >= 2; profiles/r05_ab_ex2_regs.txt records both.)
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
@@ -139,6 +141,33 @@ DEV void fft512_x2_early(C2 (*d)[8], C2 *xb, const TW &T, int t, const uint32_t 
     kpre[2] = slot_t[1024];
     kpre[3] = slot_t[1088];
     __builtin_amdgcn_sched_barrier(0);
+    passBC<INV, FU>(d[1], wc_);
+}
+
+// VAR 13: the pair with transform 0's exchange 2 in registers and transform 1's through LDS, its
+// LDS round trip running under transform 0's register moves and last pass.
+template <bool INV, bool FU, class TW, bool KO = false>
+DEV void fft512_x2_half(C2 (*d)[8], C2 *xb, const TW &T, int t) {
+    C2 wb_[7], wc_[7];
+    passA<INV, FU>(d[0], T.a);
+    ex1_write(d[0], xb, t);
+    wave_sync();
+    passA<INV, FU>(d[1], T.a);
+    ex1_read(d[0], xb, t);
+    ex1_write(d[1], xb, t);
+    wave_sync();
+    T.pass_b(wb_, t);
+    passBC<INV, FU>(d[0], wb_);
+    ex1_read(d[1], xb, t);
+    wave_sync();
+    passBC<INV, FU>(d[1], wb_);
+    ex2_write(d[1], xb, t);
+    wave_sync();
+    if (!KO) ex2_regs(d[0]);  // KO (VAR 14, timing only, wrong words): transform 0's exchange 2 skipped
+    T.pass_c(wc_, t);
+    passBC<INV, FU>(d[0], wc_);
+    ex2_read(d[1], xb, t);
+    wave_sync();
     passBC<INV, FU>(d[1], wc_);
 }
 
@@ -322,7 +351,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
             for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[16 + q], (unsigned long long)lp.acc[q]);
 #endif
         report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
-        if (FU && VAR != 10) near_tie_flag(P, near, g, valid);  // VAR 10: garbage values, no recompute
+        if (FU && VAR != 10 && VAR != 14) near_tie_flag(P, near, g, valid);  // VAR 10/14: garbage values
         if (!valid) return;
         // the b parts of the outputs (accB: coefficient t + 64m)
         if (out_mode == BR_OUT_LV1) {
@@ -442,6 +471,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
                     fft512_x2_ex2r<false, FU>(d, X, T, t);
                 else if (VAR == 10)
                     fft512_x2_noex2<false, FU>(d, X, T, t);
+                else if (VAR == 13)
+                    fft512_x2_half<false, FU>(d, X, T, t);
+                else if (VAR == 14)
+                    fft512_x2_half<false, FU, LdsTw, true>(d, X, T, t);
                 else if (VAR != 11)
                     fft512_x2<false, true, FU>(d, X, T, t);
             }
@@ -479,7 +512,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
         for (int q = 0; q < 10; q++) atomicAdd(&g_phase_cycles[q], (unsigned long long)pp.acc[q]);
 #endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
-    if (FU && VAR != 10) near_tie_flag(P, near, g, valid);  // VAR 10: garbage values, no recompute
+    if (FU && VAR != 10 && VAR != 14) near_tie_flag(P, near, g, valid);  // VAR 10/14: garbage values
     if (!valid) return;
     // the a parts of the outputs from the acc_a copy (the loader writes b's)
     if (out_mode == BR_OUT_LV1) {  // sampleExtractIndex(acc, 0): p[0] = a[0], p[j] = -a[N-j]; p[N] = b[0]: loader
@@ -560,6 +593,16 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 12>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,12> (row 5 on the loader as VAR 5, pair 1 exchange 2 in registers)";
+        break;
+    case 13:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 13>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,13> (forward pairs: one exchange 2 in registers, one in LDS)";
+        break;
+    case 14:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 14>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,14> (knock-out: one exchange 2 per forward pair skipped, wrong words)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
