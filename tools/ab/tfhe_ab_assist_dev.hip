@@ -15,7 +15,8 @@
 // VAR 11 = VAR 0 with the slot counter and the MAC's first BK group read under the pair's last pass;
 // VAR 12 = VAR 5 with pair 1's exchange 2 in registers; VAR 13 = VAR 0 with each forward pair's
 // transform 0 exchanging stage 2 in registers and transform 1 through LDS; VAR 14 = knock-out
-// timing build: VAR 13 with transform 0's exchange 2 skipped (wrong words).  (Until this fix VAR 6-10 also carried
+// timing build: VAR 13 with transform 0's exchange 2 skipped (wrong words); VAR 15 / 16 = VAR 0 with
+// the odd gate waves started ~2 k / ~4 k cycles late (exchange bursts interleaved across gates).  (Until this fix VAR 6-10 also carried
 // VAR 5's row-5 split: R5 was VAR >= 2; profiles/r05_ab_ex2_regs.txt records both.)
 #include "../../zig-tfhe_amd/csrc/tfhe_device.hpp"
 
@@ -393,6 +394,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     uint32_t near = NEAR_NONE, fail = 0;
     PhaseProf pp;  // tools/phase_prof.hip assist: 0 gather + tmp, 1 pair 0 fft, 2 pub waits, 3 macs, 4 tB wait, 5 pairs 1-2 fft, 6 fb hand-off, 7 inverse a
     pp.start();
+    // VAR 15 / 16: odd gate waves start ~2 k / ~4 k cycles late, so the four gates' LDS exchange
+    // bursts interleave instead of coinciding (the slot protocol keeps them within two pairs)
+    if (VAR == 15 && (gi & 1)) __builtin_amdgcn_s_sleep(32);
+    if (VAR == 16 && (gi & 1)) __builtin_amdgcn_s_sleep(64);
     for (int i = 0; i < n; i++) {
         pp.mark(0);
         const int at = __builtin_amdgcn_readfirstlane(at_next);
@@ -603,6 +608,16 @@ hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, c
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 14>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
                            bk2, out, out_mode, B);
         if (used) *used = "k_blind_rotate_assist_dev<true,14> (knock-out: one exchange 2 per forward pair skipped, wrong words)";
+        break;
+    case 15:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 15>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,15> (odd gates start ~2 k cycles late)";
+        break;
+    case 16:
+        hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 16>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
+                           bk2, out, out_mode, B);
+        if (used) *used = "k_blind_rotate_assist_dev<true,16> (odd gates start ~4 k cycles late)";
         break;
     case 1:
         hipLaunchKernelGGL((k_blind_rotate_assist_dev<true, 1>), grid, block, 0, s, P, T, ops, in_a, in_b, idx, testvec,
