@@ -215,10 +215,17 @@ def rooflines(p, B, params, br_avg_s, kernel):
             "arithmetic": "fused multiply-add (exact-integer regime, DESIGN.md §6)" if fused else "reference expression trees",
             "reference_tree_f64_ops_per_cmux": f64_ops_per_cmux(p.L)}
     if pmc:
+        # the effective clock of the PMC's own clock pass (GRBM_GUI_ACTIVE / 8 / duration), and the
+        # fraction of the f64 issue peak AT that clock: how much of the gap to `frac` is DVFS
+        if pmc.get("clock_ghz"):
+            roof["clock_ghz"] = pmc["clock_ghz"]
+            roof["clock_provenance"] = record_provenance(PMC_PATH, pmc) + "; " + pmc.get("clock_basis", "")
+            roof["frac_at_clock"] = round(f64_rate / (VALU_F64_PEAK / 2.4 * pmc["clock_ghz"]), 4)
         roof["pmc"] = {k: pmc[k] for k in ("valu_f64_insts_per_launch", "valu_insts_per_item_per_cmux",
                                            "lds_insts_per_item_per_cmux", "valu_insts_per_gate_wave_per_cmux",
                                            "lds_insts_per_gate_wave_per_cmux", "wait_any_frac_all_waves")
                        if k in pmc}
+        roof["pmc"]["provenance"] = record_provenance(PMC_PATH, pmc)
         f64_insts = pmc.get("valu_f64_insts_per_launch", 0) + pmc.get("valu_fma_f64_insts_per_launch", 0)
         if f64_insts:
             roof["pmc"]["valu_f64_frac_from_pmc"] = round(f64_insts * 64 / br_avg_s / VALU_F64_PEAK, 4)
@@ -233,7 +240,9 @@ def rooflines(p, B, params, br_avg_s, kernel):
                                   "peak_ns_2_waves": 2.14, "frac": round(2.01 / ns, 4),
                                   "valu_insts_per_item_per_cmux": pmc.get("valu_insts_per_item_per_cmux"),
                                   "note": "issue interval achieved vs the measured sustained f64 VALU interval; "
-                                          "the kernel runs 2 waves per SIMD (gate + loader)"}
+                                          "the kernel runs 2 waves per SIMD (gate + loader)",
+                                  "provenance": "SQ_INSTS_VALU " + record_provenance(PMC_PATH, pmc)
+                                                + "; kernel time in-run (HIP events)"}
         # the DRAM side of the same kernel: measured bytes per launch / kernel time / HBM peak
         roof["dram"] = {"achieved_gbs": round(pmc["hbm_bytes_per_launch"] / br_avg_s / 1e9, 1),
                         "peak_gbs": HBM_PEAK_BPS / 1e9,
@@ -243,13 +252,20 @@ def rooflines(p, B, params, br_avg_s, kernel):
     # the same kernel's rocprofv3 --stats average, beside the HIP-event one above
     rp, rwhy = rocprof_record()
     if rp:
-        # rocprof basis: the average over the recorded launches without the slowest one (the
-        # first launch of the run, a warm-up: its code-object load and cold caches), reproducible
-        # from the committed csv as (TotalDurationNs - MaxNs) / (Calls - 1)
-        avg = rp.get("avg_ms_without_max", rp["avg_ms"])
+        # rocprof basis: with the run's kernel trace committed, the launches after bench.py's
+        # warm-up steps BY POSITION (never by dropping the slowest launch); otherwise the plain
+        # average over every recorded launch (the basis of rounds 1-4)
+        if "avg_ms_excl_warmup" in rp:
+            avg = rp["avg_ms_excl_warmup"]
+            basis = (f"the launches after the first {rp['warmup_launches_excluded']} (bench.py's warm-up steps) in "
+                     f"dispatch order, from the kernel trace {rp['trace']}")
+        else:
+            avg, basis = rp["avg_ms"], "AverageNs of the csv row: every recorded launch"
         roof["kernel_avg_ms_rocprof"] = avg
-        roof["rocprof"] = {k: rp[k] for k in ("launches", "avg_ms", "min_ms", "max_ms", "source") if k in rp}
-        roof["rocprof"]["basis"] = "(TotalDurationNs - MaxNs) / (Calls - 1) of the csv row: the warm-up launch excluded"
+        roof["rocprof"] = {k: rp[k] for k in ("launches", "avg_ms", "avg_ms_excl_warmup", "min_ms", "max_ms", "source")
+                           if k in rp}
+        roof["rocprof"]["basis"] = basis
+        roof["rocprof"]["provenance"] = record_provenance(ROCPROF_PATH, rp)
         roof["frac_rocprof"] = round(ops / (avg / 1e3) / VALU_F64_PEAK, 4)
     else:
         roof["rocprof_note"] = rwhy
@@ -261,6 +277,13 @@ def rooflines(p, B, params, br_avg_s, kernel):
     key = {"key_bytes_consumed_per_s": round(alg / br_avg_s, 0), "key_bytes_consumed_per_launch": alg,
            "note": "n*2L*2*N*8 + I/O bytes every gate consumes, / kernel time; on-chip reuse, not DRAM traffic"}
     return roof, key
+
+
+def record_provenance(path, rec) -> str:
+    """Which figures of the line are read from a committed record rather than measured in this run."""
+    return (f"from committed record {os.path.relpath(path, ROOT)} (source {rec.get('source', rec.get('method', '?'))[:60]}), "
+            f"measured in a separate profiled run, possibly on another box; matched to this binary by kernel build id "
+            f"{rec.get('kernel_build_id')}")
 
 
 def rocprof_record():

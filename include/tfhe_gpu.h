@@ -201,10 +201,15 @@ enum {
     TFHE_OPT_LEVEL_ISSUE_US = 15, /* read-only: host microseconds the last level-split circuit_eval spent
                                      issuing its per-level launches, peer copies and event waits (one
                                      host thread for all devices) */
-    TFHE_OPT_KEY_ROW_RMS_PPM = 16 /* read-only: the resident key's largest TRGSW row RMS / 2^31, in
+    TFHE_OPT_KEY_ROW_RMS_PPM = 16, /* read-only: the resident key's largest TRGSW row RMS / 2^31, in
                                      millionths (the admission's row-energy rule admits <= 650000;
                                      keygen'd keys ~600000; ABI 6) */
+    TFHE_OPT_HOST_STAGING = 17    /* host-buffer copies: 2 auto (default: pinned staging on the devices of a
+                                     multi-device context, pageable copies on a single-device one), 0 pageable
+                                     hipMemcpyAsync from / to the caller's buffers, 1 through per-device pinned
+                                     staging (host memcpy + DMA).  Same words either way */
 };
+enum { TFHE_STAGING_PAGEABLE = 0, TFHE_STAGING_PINNED = 1, TFHE_STAGING_AUTO = 2 };  /* TFHE_OPT_HOST_STAGING */
 /* TFHE_ARITH_AUTO (default): at the L=3 / Bg=2^6 sets the blind rotation
  * runs fused multiply-adds in the reference's operation order, with a margin
  * guard: every value it rounds must lie within 1/4 of an integer; an item
@@ -421,7 +426,10 @@ int tfhe_reenc_key_gen_asymmetric(const tfhe_params *params, const uint32_t *key
                                   uint32_t *out);
 /* Generator.generateLookupTableAssign (lut/generator.zig:85-135): testvec
  * (2N words, a = 0) for f given as a table f_table[x], x < m, encoded by
- * Encoder.new(m) (scale 1/(2m), encoder.zig:29-42).  Any m >= 1. */
+ * Encoder.new(m) (scale 1/(2m), encoder.zig:29-42).  1 <= m <= TFHE_LUT_MAX_M
+ * (TFHE_ERR_INVALID outside; m > N leaves some messages' ranges empty, as the
+ * reference's divRound ranges do).  testvec must hold 2N words. */
+#define TFHE_LUT_MAX_M (1u << 24)
 int tfhe_lut_generate(const tfhe_params *params, uint32_t m, const uint32_t *f_table,
                       uint32_t *testvec);
 /* The same with Encoder.withScale(m, scale) (Generator.withScale, generateLookupTableCustom;

@@ -48,11 +48,21 @@ def test_roofline_from_committed_records(monkeypatch):
     ops = 145424 * 700 * 1024
     assert roof["algorithmic_f64_ops_per_launch"] == ops
     assert roof["frac"] == pytest.approx(ops / kernel_s / bench.VALU_F64_PEAK, abs=1e-4)
-    # rocprof basis: (TotalDurationNs - MaxNs) / (Calls - 1) of the csv row named in the record
+    # rocprof basis: the launches after the warm-up steps BY POSITION from the committed
+    # kernel trace when the record names one, else the csv row's plain average over every launch
     src = os.path.join(ROOT, rp["source"])
     row = next(r for r in csv.DictReader(open(src)) if r["Name"].startswith(rp["kernel"] + "("))
-    avg_ms = (float(row["TotalDurationNs"]) - float(row["MaxNs"])) / (int(row["Calls"]) - 1) / 1e6
+    if "trace" in rp:
+        ds = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]) - int(x["Start_Timestamp"]))
+                    for x in csv.DictReader(open(os.path.join(ROOT, rp["trace"])))
+                    if x["Kernel_Name"].split("(")[0] == rp["kernel"])
+        assert len(ds) == int(row["Calls"])
+        kept = [d for _, d in ds[rp["warmup_launches_excluded"]:]]
+        avg_ms = sum(kept) / len(kept) / 1e6
+    else:
+        avg_ms = float(row["AverageNs"]) / 1e6
     assert roof["kernel_avg_ms_rocprof"] == pytest.approx(avg_ms, abs=1e-3)
+    assert "committed record" in roof["rocprof"]["provenance"] and "committed record" in roof["pmc"]["provenance"]
     assert roof["frac_rocprof"] == pytest.approx(ops / (avg_ms / 1e3) / bench.VALU_F64_PEAK, abs=1e-4)
     # VALU issue: wave-instructions per SIMD per launch against the kernel time
     ns = kernel_s * 1e9 / (pmc["raw_per_launch"]["SQ_INSTS_VALU"] / 1024)
@@ -62,3 +72,21 @@ def test_roofline_from_committed_records(monkeypatch):
     raw = pmc["raw_per_launch"]
     assert roof["traffic"] == int(raw["FETCH_SIZE"] * 1024 * 2 + raw["WRITE_SIZE"] * 1024)
     assert key["key_bytes_consumed_per_launch"] == bench.algorithmic_bytes_per_gate(p) * 1024
+
+
+def test_clock_and_frac_at_clock_from_committed_pmc(monkeypatch):
+    """roofline.clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / the clock pass's kernel duration, and
+    frac_at_clock = achieved / (1,024 SIMDs x 16 lanes x clock), both from the committed PMC file."""
+    pmc = json.load(open(bench.PMC_PATH))
+    if "clock_ghz" not in pmc:
+        pytest.skip("the committed PMC record predates the clock pass")
+    monkeypatch.setattr(bench, "kernel_build_id", lambda: pmc["kernel_build_id"])
+    clk = pmc["raw_per_launch"]["GRBM_GUI_ACTIVE"] / 8 / pmc["clock_pass_kernel_ns"]
+    assert pmc["clock_ghz"] == pytest.approx(clk, abs=1e-3)
+    p = tfhe_amd.make_params("128")
+    kernel_s = 5.97e-3
+    roof, _ = bench.rooflines(p, 1024, "128", kernel_s, "k_blind_rotate_assist<true> (whole form, fused)")
+    ops = 145424 * 700 * 1024
+    assert roof["clock_ghz"] == pmc["clock_ghz"]
+    assert roof["frac_at_clock"] == pytest.approx(ops / kernel_s / (1024 * 16 * clk * 1e9), abs=1e-4)
+    assert roof["frac_at_clock"] >= roof["frac"] - 1e-9 or clk > 2.4

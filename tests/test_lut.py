@@ -114,3 +114,48 @@ def test_table_ranges_follow_div_round(oracle):
     owner = [x for x in range(m) if oracle.div_round(x * N, m) < oracle.div_round((x + 1) * N, m)]
     assert owner == list(range(0, m, 2))
     assert np.array_equal(tv, vals[owner])
+
+
+# ---- argument checks at the boundary --------------------------------
+def test_short_table_is_refused_before_the_c_call():
+    """The C side writes 2N words: a LookupTable of any other size never reaches it."""
+    with pytest.raises(ValueError):
+        tfhe_amd.LookupTable.from_poly(np.zeros(16, np.uint32))
+    small = tfhe_amd.LookupTable.new(N=8)  # a valid 16-word table, but the generator's params have N = 1024
+    with pytest.raises(ValueError):
+        tfhe_amd.Generator.new(4).generate_lookup_table_assign(lambda x: x, small)
+    lut = tfhe_amd.LookupTable.new()
+    lut.poly = np.zeros(2 * N, np.uint64)  # right size, wrong word type
+    with pytest.raises(ValueError):
+        tfhe_amd.Generator.new(4).generate_lookup_table_full_assign(lambda x: x, lut)
+    lut.poly = np.zeros(4 * N, np.uint32)[::2]  # right size and type, not contiguous
+    with pytest.raises(ValueError):
+        tfhe_amd.Generator.new(4).generate_lookup_table_assign(lambda x: x, lut)
+
+
+def test_function_values_past_32_bits_reduce_mod_m_first(oracle):
+    """Encoder.encode reduces the usize f(x) mod m (encoder.zig:66-74): f(x) >= 2^32
+    with m not a power of two gives (f(x) mod m), not (f(x) mod 2^32) mod m."""
+    m = 7
+    f = [(1 << 40) + 3 * x for x in range(m)]
+    got = tfhe_amd.Generator.new(m).generate_lookup_table(lambda x: f[x]).poly
+    want = oracle.lut_generate(N, m, np.array([v % m for v in f], np.uint32))
+    assert np.array_equal(got, want)
+    assert not np.array_equal(got, oracle.lut_generate(N, m, np.array([v & MAX_U32 for v in f], np.uint32)))
+
+
+def test_huge_message_modulus_is_an_error_not_an_abort():
+    """m is bounded (TFHE_LUT_MAX_M); m = 2^32 - 1 returns TFHE_ERR_INVALID from every entry."""
+    import ctypes as C
+    lib = tfhe_amd.load_library()
+    p = tfhe_amd.make_params("128")
+    tab = np.zeros(4, np.uint32)
+    out = np.zeros(2 * N, np.uint32)
+    u32p = C.POINTER(C.c_uint32)
+    for call in (lambda m: lib.tfhe_lut_generate(C.byref(p), m, tab.ctypes.data_as(u32p), out.ctypes.data_as(u32p)),
+                 lambda m: lib.tfhe_lut_generate_scaled(C.byref(p), m, 0.5, tab.ctypes.data_as(u32p),
+                                                        out.ctypes.data_as(u32p)),
+                 lambda m: lib.tfhe_lut_generate_full(C.byref(p), m, tab.ctypes.data_as(u32p),
+                                                      out.ctypes.data_as(u32p))):
+        assert call(0xFFFFFFFF) == -1
+        assert call((1 << 24) + 1) == -1

@@ -321,3 +321,33 @@ def test_lut_dev_refuses_multi_device_context(oracle):
         multi.bootstrap_lut_batch_dev(64, 64, 64, 1)  # never dereferenced: refused first
     assert e.value.status == tfhe_amd.ERR_INVALID and "single-device" in str(e.value)
     multi.close()
+
+
+def test_host_staging_modes_same_words(oracle):
+    """TFHE_OPT_HOST_STAGING (round 6): the host-buffer entries of an
+    8-shard context through pageable copies (0), per-device pinned staging (1) and the
+    default (2 = auto: pinned on a multi-device context) give the same words as one
+    device, on a ragged gate batch, a bootstrap batch and a blind rotation (TRLWE
+    outputs, the largest D2H); a single-device context stays pageable under auto."""
+    single, k = loaded(oracle, "80")
+    multi, _ = loaded(oracle, "80", devices=[0] * 8)
+    assert multi.get_option("host_staging") == tfhe_amd.STAGING_AUTO
+    g = rng(83)
+    B = 1030
+    ops = g.integers(0, 10, B).astype(np.uint8)
+    A, Bc = u32rand(g, B, k.p.n + 1), u32rand(g, B, k.p.n + 1)
+    want = single.gate_batch(ops, A, Bc)
+    want_bs = single.bootstrap_batch(A[:77])
+    want_br = single.blind_rotate_batch(Bc[:40])
+    for mode in (tfhe_amd.STAGING_PAGEABLE, tfhe_amd.STAGING_PINNED, tfhe_amd.STAGING_AUTO):
+        with multi.options(host_staging=mode):
+            for _ in range(2):  # the arena reused from offset 0 after each synchronisation
+                assert np.array_equal(multi.gate_batch(ops, A, Bc), want), mode
+            assert np.array_equal(multi.bootstrap_batch(A[:77]), want_bs), mode
+            assert np.array_equal(multi.blind_rotate_batch(Bc[:40]), want_br), mode
+    with single.options(host_staging=tfhe_amd.STAGING_PINNED):  # forced on one device
+        assert np.array_equal(single.gate_batch(ops, A, Bc), want)
+    idx = np.array([0, 129, 903, B - 1])
+    assert np.array_equal(want[idx], oracle.gate_batch(k.p, ops[idx], A[idx], Bc[idx], k.ck, threads=4))
+    single.close()
+    multi.close()

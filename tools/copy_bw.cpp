@@ -4,6 +4,7 @@
 //   hipcc -O2 -o tools/bin/copy_bw tools/copy_bw.cpp -lpthread && tools/bin/copy_bw
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -103,6 +104,72 @@ int main() {
             }
             std::printf("concurrent pageable %.1f MB, %d thread(s)/stream(s): H2D %.3f ms (%.1f GB/s), D2H %.3f ms (%.1f GB/s)\n",
                         in_bytes / 1e6, th, best_h * 1e3, rate(in_bytes, best_h), best_d * 1e3, rate(in_bytes, best_d));
+        }
+    }
+    // Round 6: the multi-device host path's per-shard copies.  T host
+    // threads, each one shard of 1,024 gates (H2D a + b, 2 x 2.87 MB; D2H out, 2.87 MB) on its own
+    // stream and its own caller buffers, three ways: pageable hipMemcpyAsync from the caller's
+    // buffer; pinned staging (host memcpy into the shard's own pinned arena, then the DMA; the
+    // library's TFHE_OPT_HOST_STAGING = 1); hipHostRegister of the caller's slice for the call
+    // (register, DMA, unregister).  One device here, so the DMAs of all shards share one link:
+    // per-shard wall time at T threads is an upper bound on what T distinct devices would see.
+    {
+        const size_t a_bytes = 1024 * 701 * 4;
+        const int T = 8;
+        std::vector<std::vector<char>> ca(T, std::vector<char>(a_bytes, 1)), cb(T, std::vector<char>(a_bytes, 2)),
+            co(T, std::vector<char>(a_bytes, 0));
+        std::vector<char *> pin(T), pout(T), dv(T);
+        std::vector<hipStream_t> ss(T);
+        for (int k = 0; k < T; k++) {
+            CK(hipHostMalloc((void **)&pin[k], 2 * a_bytes, hipHostMallocDefault));
+            CK(hipHostMalloc((void **)&pout[k], a_bytes, hipHostMallocDefault));
+            CK(hipMalloc((void **)&dv[k], 3 * a_bytes));
+            CK(hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking));
+        }
+        const char *names[3] = {"pageable", "pinned staging", "hipHostRegister"};
+        for (int th : {1, 2, 4, 8}) {
+            for (int mode = 0; mode < 3; mode++) {
+                std::vector<double> walls;
+                for (int rep = 0; rep < 7; rep++) {
+                    double t0 = now();
+                    std::vector<std::thread> v;
+                    for (int k = 0; k < th; k++)
+                        v.emplace_back([&, k] {
+                            char *d = dv[k];
+                            if (mode == 0) {
+                                (void)hipMemcpyAsync(d, ca[k].data(), a_bytes, hipMemcpyHostToDevice, ss[k]);
+                                (void)hipMemcpyAsync(d + a_bytes, cb[k].data(), a_bytes, hipMemcpyHostToDevice, ss[k]);
+                                (void)hipMemcpyAsync(co[k].data(), d + 2 * a_bytes, a_bytes, hipMemcpyDeviceToHost, ss[k]);
+                                (void)hipStreamSynchronize(ss[k]);
+                            } else if (mode == 1) {
+                                std::memcpy(pin[k], ca[k].data(), a_bytes);
+                                (void)hipMemcpyAsync(d, pin[k], a_bytes, hipMemcpyHostToDevice, ss[k]);
+                                std::memcpy(pin[k] + a_bytes, cb[k].data(), a_bytes);
+                                (void)hipMemcpyAsync(d + a_bytes, pin[k] + a_bytes, a_bytes, hipMemcpyHostToDevice, ss[k]);
+                                (void)hipMemcpyAsync(pout[k], d + 2 * a_bytes, a_bytes, hipMemcpyDeviceToHost, ss[k]);
+                                (void)hipStreamSynchronize(ss[k]);
+                                std::memcpy(co[k].data(), pout[k], a_bytes);
+                            } else {
+                                (void)hipHostRegister(ca[k].data(), a_bytes, hipHostRegisterDefault);
+                                (void)hipHostRegister(cb[k].data(), a_bytes, hipHostRegisterDefault);
+                                (void)hipHostRegister(co[k].data(), a_bytes, hipHostRegisterDefault);
+                                (void)hipMemcpyAsync(d, ca[k].data(), a_bytes, hipMemcpyHostToDevice, ss[k]);
+                                (void)hipMemcpyAsync(d + a_bytes, cb[k].data(), a_bytes, hipMemcpyHostToDevice, ss[k]);
+                                (void)hipMemcpyAsync(co[k].data(), d + 2 * a_bytes, a_bytes, hipMemcpyDeviceToHost, ss[k]);
+                                (void)hipStreamSynchronize(ss[k]);
+                                (void)hipHostUnregister(ca[k].data());
+                                (void)hipHostUnregister(cb[k].data());
+                                (void)hipHostUnregister(co[k].data());
+                            }
+                        });
+                    for (auto &x : v) x.join();
+                    walls.push_back(now() - t0);
+                }
+                std::sort(walls.begin(), walls.end());
+                const double med = walls[walls.size() / 2], bytes = 3.0 * a_bytes * th;
+                std::printf("shards %d x 1,024 gates (8.6 MB each), %-15s: median %.3f ms (min %.3f), %.1f GB/s total\n",
+                            th, names[mode], med * 1e3, walls[0] * 1e3, bytes / med / 1e9);
+            }
         }
     }
     return 0;

@@ -20,6 +20,33 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def clock_from_grbm(d, kernel):
+    """{'clock_ghz', 'clock_basis'} from the pass holding GRBM_GUI_ACTIVE and a kernel trace, or None."""
+    for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+        rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].split("(")[0] == kernel
+                and r["Counter_Name"] == "GRBM_GUI_ACTIVE"]
+        if not rows:
+            continue
+        # the dispatch's duration: the kernel trace of the same run if it was collected, else
+        # the counter rows' own dispatch timestamps
+        tr = glob.glob(os.path.join(os.path.dirname(f), "run_kernel_trace.csv"))
+        src = csv.DictReader(open(tr[0])) if tr else rows
+        dur = {r["Dispatch_Id"]: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+               for r in src if r["Kernel_Name"].split("(")[0] == kernel}
+        act = collections.defaultdict(float)
+        for r in rows:
+            act[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        pairs = [(act[k], dur[k]) for k in act if k in dur and dur[k] > 0]
+        if not pairs:
+            continue
+        a, ns = sum(p[0] for p in pairs), sum(p[1] for p in pairs)
+        return {"clock_ghz": round(a / 8 / ns, 4), "grbm_gui_active_per_launch": a / len(pairs),
+                "clock_pass_kernel_ns": ns / len(pairs),
+                "clock_basis": "GRBM_GUI_ACTIVE / 8 XCDs / the dispatch's kernel-trace duration, in a profiled "
+                               "pass of its own (profiled passes clock lower than unprofiled runs)"}
+    return None
+
+
 def main():
     d = sys.argv[1]
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
@@ -75,6 +102,11 @@ def main():
         rec["wait_any_frac_all_waves"] = round(per["SQ_WAIT_ANY"] / per["SQ_WAVE_CYCLES"], 4)
     if "SQ_ACTIVE_INST_VALU" in per and "SQ_WAVE_CYCLES" in per:
         rec["valu_active_frac_all_waves"] = round(per["SQ_ACTIVE_INST_VALU"] / per["SQ_WAVE_CYCLES"], 4)
+    # effective clock (MI355X_MICROARCH.md, DVFS give-back): GRBM_GUI_ACTIVE is summed over the 8 XCDs;
+    # the pass that collected it also ran --kernel-trace, which gives the same dispatch's duration
+    clk = clock_from_grbm(d, name)
+    if clk:
+        rec.update(clk)
     out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles", "pmc_blind_rotate.json")
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))

@@ -19,6 +19,7 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <new>
 #include <vector>
 
 #include "host_math.hpp"
@@ -148,6 +149,12 @@ struct tfhe_gpu_ctx {
     size_t pin_in_bytes = 0, pin_out_bytes = 0;
     std::unique_ptr<WorkerPool> workers;
     int64_t pipeline = 0;  // TFHE_OPT_HOST_PIPELINE (off by default: measured slower)
+    // host-buffer copies through pinned staging (TFHE_OPT_HOST_STAGING; h2d / d2h_sync): the
+    // arena's bytes in use since the last synchronisation of this context's stream
+    int64_t host_staging = TFHE_STAGING_AUTO;
+    bool in_multi = false;  // a device of a multi-device context (auto staging: pinned)
+    char *stage_in = nullptr, *stage_out = nullptr;
+    size_t stage_in_bytes = 0, stage_out_bytes = 0, stage_used = 0;
     std::vector<ncclComm_t> comms;   // one communicator per shard, created on the first key broadcast
 };
 
@@ -321,10 +328,46 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
     return TFHE_OK;
 }
 
+bool staged(const tfhe_gpu_ctx *c) {
+    return c->host_staging == TFHE_STAGING_PINNED || (c->host_staging == TFHE_STAGING_AUTO && c->in_multi);
+}
+
+// Pinned host buffer of at least `bytes` (grown by doubling; nothing may be in flight from it).
+int ensure_stage(tfhe_gpu_ctx *c, char *&p, size_t &have, size_t bytes) {
+    if (have >= bytes) return TFHE_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    have = 0;
+    const size_t want = std::max(bytes, (size_t)1 << 20);
+    HIPCHK(c, hipHostMalloc((void **)&p, want, hipHostMallocDefault));
+    have = want;
+    return TFHE_OK;
+}
+
+// Host -> device into `buf`.  Pageable: one hipMemcpyAsync from the caller's buffer.  Staged
+// (TFHE_OPT_HOST_STAGING): a host memcpy into this context's pinned arena, then the DMA from
+// there, so concurrent shards' copies do not go through the runtime's pageable staging
+// (measured serialised across host threads).  The arena is reused from
+// offset 0 after every synchronisation of the stream (d2h_sync); when it is full the stream
+// is synchronised first, so no copy in flight ever reads overwritten bytes.
 int h2d(tfhe_gpu_ctx *c, DevBuf &buf, const void *src, size_t bytes) {
     int rc = ensure(c, buf, bytes);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    if (!staged(c) || !bytes) {
+        HIPCHK(c, hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        return TFHE_OK;
+    }
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (c->stage_used + need > c->stage_in_bytes) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->stage_used = 0;
+        rc = ensure_stage(c, c->stage_in, c->stage_in_bytes, std::max(need, 2 * c->stage_in_bytes));
+        if (rc) return rc;
+    }
+    char *p = c->stage_in + c->stage_used;
+    std::memcpy(p, src, bytes);
+    HIPCHK(c, hipMemcpyAsync(buf.p, p, bytes, hipMemcpyHostToDevice, c->stream));
+    c->stage_used += need;
     return TFHE_OK;
 }
 
@@ -433,6 +476,15 @@ int key_admission(tfhe_gpu_ctx *c) {
 int d2h_sync(tfhe_gpu_ctx *c, void *dst, const void *src, size_t bytes) {
     int rc = queue_err_copy(c);
     if (rc) return rc;
+    if (staged(c) && bytes) {  // DMA into the pinned arena, one synchronisation, then a host memcpy
+        rc = ensure_stage(c, c->stage_out, c->stage_out_bytes, bytes);
+        if (rc) return rc;
+        HIPCHK(c, hipMemcpyAsync(c->stage_out, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->stage_used = 0;  // every staged H2D of the call has landed
+        std::memcpy(dst, c->stage_out, bytes);
+        return check_err_word(c);
+    }
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     // a pageable destination makes the copy synchronous: the stream is idle by
     // now and hipStreamQuery says so at once, where hipStreamSynchronize on an
@@ -615,6 +667,8 @@ void tfhe_gpu_destroy(tfhe_gpu_ctx *c) {
     if (c->pipe_ev) (void)hipEventDestroy(c->pipe_ev);
     if (c->pin_in) (void)hipHostFree(c->pin_in);
     if (c->pin_out) (void)hipHostFree(c->pin_out);
+    if (c->stage_in) (void)hipHostFree(c->stage_in);
+    if (c->stage_out) (void)hipHostFree(c->stage_out);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->stream_ev) (void)hipEventDestroy(c->stream_ev);
     delete c;
@@ -1763,22 +1817,30 @@ static void lut_from_values(size_t N, size_t m, const uint32_t *values, uint32_t
 }
 
 int tfhe_lut_generate_scaled(const tfhe_params *p, uint32_t m, double scale, const uint32_t *f_table, uint32_t *tv) {
-    if (!p || !f_table || !tv || m == 0) return TFHE_ERR_INVALID;
-    std::vector<uint32_t> enc(m);
-    for (uint32_t x = 0; x < m; x++)  // Encoder.encode (encoder.zig:66-74): (f(x) mod m) * scale -> torus
-        enc[x] = host::f64_to_torus((double)(f_table[x] % m) * scale);
-    lut_from_values(p->N, m, enc.data(), tv);
+    if (!p || !f_table || !tv || m == 0 || m > TFHE_LUT_MAX_M) return TFHE_ERR_INVALID;
+    try {
+        std::vector<uint32_t> enc(m);
+        for (uint32_t x = 0; x < m; x++)  // Encoder.encode (encoder.zig:66-74): (f(x) mod m) * scale -> torus
+            enc[x] = host::f64_to_torus((double)(f_table[x] % m) * scale);
+        lut_from_values(p->N, m, enc.data(), tv);
+    } catch (const std::bad_alloc &) {  // never through the C ABI (std::terminate)
+        return TFHE_ERR_OOM;
+    }
     return TFHE_OK;
 }
 
 int tfhe_lut_generate(const tfhe_params *p, uint32_t m, const uint32_t *f_table, uint32_t *tv) {
-    if (!p || m == 0) return TFHE_ERR_INVALID;
+    if (!p || m == 0 || m > TFHE_LUT_MAX_M) return TFHE_ERR_INVALID;
     return tfhe_lut_generate_scaled(p, m, 1.0 / (2.0 * (double)m), f_table, tv);  // Encoder.new (encoder.zig:29-42)
 }
 
 int tfhe_lut_generate_full(const tfhe_params *p, uint32_t m, const uint32_t *values, uint32_t *tv) {
-    if (!p || !values || !tv || m == 0) return TFHE_ERR_INVALID;
-    lut_from_values(p->N, m, values, tv);
+    if (!p || !values || !tv || m == 0 || m > TFHE_LUT_MAX_M) return TFHE_ERR_INVALID;
+    try {
+        lut_from_values(p->N, m, values, tv);
+    } catch (const std::bad_alloc &) {
+        return TFHE_ERR_OOM;
+    }
     return TFHE_OK;
 }
 
@@ -1816,6 +1878,7 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     case TFHE_OPT_BR_SPIN_CAP: ok = v >= 0 && v <= 0xFFFFFFFFll; break;
     case TFHE_OPT_HOST_PIPELINE: ok = v == 0 || v == 1; break;
     case TFHE_OPT_CIRCUIT_SPLIT: ok = v >= 0 && v <= 2; break;
+    case TFHE_OPT_HOST_STAGING: ok = v == TFHE_STAGING_PAGEABLE || v == TFHE_STAGING_PINNED || v == TFHE_STAGING_AUTO; break;
     case TFHE_OPT_TWIDDLES:
         ok = v == TFHE_TWIDDLES_GLIBC || v == TFHE_TWIDDLES_FDLIBM;
         // tfhe_gpu_keygen transformed the resident BK with the current tables:
@@ -1850,6 +1913,11 @@ int apply_option(tfhe_gpu_ctx *c, int key, int64_t v) {
     case TFHE_OPT_BR_SPIN_CAP: c->K.spin_cap = (uint32_t)v; break;
     case TFHE_OPT_HOST_PIPELINE: c->pipeline = v; break;
     case TFHE_OPT_CIRCUIT_SPLIT: c->circuit_split = v; break;
+    case TFHE_OPT_HOST_STAGING:
+        if (c->stage_used) HIPCHK(c, hipStreamSynchronize(c->stream));  // nothing in flight from the arena
+        c->stage_used = 0;
+        c->host_staging = v;
+        break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;
@@ -1891,6 +1959,7 @@ int tfhe_gpu_get_option(const tfhe_gpu_ctx *c, int key, int64_t *v) {
     case TFHE_OPT_BR_SPIN_CAP: *v = c->K.spin_cap; break;
     case TFHE_OPT_HOST_PIPELINE: *v = c->pipeline; break;
     case TFHE_OPT_CIRCUIT_SPLIT: *v = c->circuit_split; break;
+    case TFHE_OPT_HOST_STAGING: *v = c->host_staging; break;
     default: return TFHE_ERR_INVALID;
     }
     return TFHE_OK;
@@ -2363,6 +2432,8 @@ int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int 
         }
         root->shards.push_back(s);
     }
+    if (num_devices > 1)
+        for (tfhe_gpu_ctx *s : root->shards) s->in_multi = true;  // auto host staging: pinned
     std::vector<int> sorted = devs;
     std::sort(sorted.begin(), sorted.end());
     root->distinct_devices = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();

@@ -24,11 +24,11 @@ LIB_PATH = os.environ.get("TFHE_GPU_LIB") or os.path.join(HERE, "lib", "libtfhe_
 # tfhe_gpu_set_option keys / values (include/tfhe_gpu.h TFHE_OPT_*, TFHE_TWIDDLES_*)
 OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_groups": 5, "ks_sel_items": 6,
            "circuit_pack": 7, "twiddles": 8, "arith": 9, "br_sync": 10, "br_spin_cap": 11, "host_pipeline": 12,
-           "circuit_split": 13}
+           "circuit_split": 13, "host_staging": 17}
 READONLY_OPTIONS = {"fused_admitted": 14, "level_issue_us": 15, "key_row_rms_ppm": 16}  # tfhe_gpu_get_option only
 OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 3, "ks_narrow": 0, "ks_item_groups": 0,
                    "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1, "br_spin_cap": 0,
-                   "host_pipeline": 0, "circuit_split": 0}
+                   "host_pipeline": 0, "circuit_split": 0, "host_staging": 2}
 # status codes (include/tfhe_gpu.h TFHE_ERR_*)
 ERR_INVALID, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_IO, ERR_DEVICE = -1, -2, -3, -4, -5, -6
 # 2 split, 4 pair: removed (round 4); 6 duo, 7 wide2: A/B libraries only (tools/ab/, round 5); 5 octo: L = 1
@@ -36,6 +36,7 @@ BR_FORMS = {"auto": 0, "whole": 1, "wide": 3, "octo": 5, "duo": 6, "wide2": 7, "
 BUILD_PRODUCT, BUILD_AB = 0, 1  # tfhe_gpu_build_kind
 TWIDDLES_GLIBC, TWIDDLES_FDLIBM = 0, 1
 ARITH_AUTO, ARITH_REFERENCE, ARITH_FUSED_FORCED = 0, 1, 2
+STAGING_PAGEABLE, STAGING_PINNED, STAGING_AUTO = 0, 1, 2  # TFHE_OPT_HOST_STAGING
 
 # gate op codes, include/tfhe_gpu.h TFHE_GATE_* (gates.zig:48-121)
 NAND, OR, AND, XOR, XNOR, NOR, ANDNY, ANDYN, ORNY, ORYN = range(10)
@@ -752,14 +753,16 @@ class LookupTable:
 
     def __init__(self, poly=None, N: int = 1024):
         self.poly = np.zeros(2 * N, np.uint32) if poly is None else np.array(poly, np.uint32).reshape(-1)
+        if self.poly.size != 2 * int(N):
+            raise ValueError(f"LookupTable: a TRLWELv1 has 2N = {2 * int(N)} words (a ++ b), got {self.poly.size}")
 
     @classmethod
     def new(cls, N: int = 1024) -> "LookupTable":  # :23-27
         return cls(N=N)
 
     @classmethod
-    def from_poly(cls, poly) -> "LookupTable":  # :33-35 (a copy of the TRLWELv1's words)
-        return cls(poly)
+    def from_poly(cls, poly, N: int = 1024) -> "LookupTable":  # :33-35 (a copy of the TRLWELv1's words)
+        return cls(poly, N)
 
     @property
     def a(self):
@@ -809,9 +812,20 @@ class Generator:
     def lookup_table_size(self) -> int:  # :240-242
         return self.lookup_table_size_
 
+    def _check_lut(self, lut: LookupTable):
+        """The C side writes 2N words into lut.poly: refuse anything else before the call."""
+        p = lut.poly
+        if not (isinstance(p, np.ndarray) and p.dtype == np.uint32 and p.flags.c_contiguous
+                and p.size == 2 * int(self.params.N)):
+            raise ValueError(f"LookupTable.poly must be a C-contiguous uint32 array of 2N = {2 * int(self.params.N)} "
+                             f"words for these params, got {getattr(p, 'dtype', type(p))} of size {getattr(p, 'size', '?')}")
+
     def generate_lookup_table_assign(self, f, lut: LookupTable):  # :85-135
+        self._check_lut(lut)
         m = self.encoder.message_modulus
-        table = np.array([f(x) for x in range(m)], dtype=np.uint32)
+        # Encoder.encode reduces f(x) (a usize) mod m in 64 bits (encoder.zig:66-74): reduce in
+        # Python first, so f(x) >= 2^32 neither overflows the uint32 table nor wraps before the mod
+        table = np.array([int(f(x)) % m for x in range(m)], dtype=np.uint32)
         rc = load_library().tfhe_lut_generate_scaled(C.byref(self.params), m, self.encoder.scale,
                                                      table.ctypes.data_as(u32p), lut.poly.ctypes.data_as(u32p))
         if rc:
@@ -823,6 +837,7 @@ class Generator:
         return lut
 
     def generate_lookup_table_full_assign(self, f, lut: LookupTable):  # :155-191: f(x) is a Torus value
+        self._check_lut(lut)
         m = self.encoder.message_modulus
         vals = np.array([int(f(x)) & 0xFFFFFFFF for x in range(m)], dtype=np.uint32)
         rc = load_library().tfhe_lut_generate_full(C.byref(self.params), m, vals.ctypes.data_as(u32p),
