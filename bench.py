@@ -743,9 +743,10 @@ def main():
                                       "untimed pass of profiled_steps steps after the timed region, HIP events "
                                       "around each launch on its stream; the timed steps carry no events"},
             "margin_guard": {"recomputed_items": recomputed, "items": B * args.steps,
-                             "note": "fused arithmetic; items that round a value 1/4 or more off its integer are "
-                                     "redone in the reference's expression trees inside the timed launches "
-                                     "(DESIGN.md §6.1)"},
+                             "note": ("fused arithmetic; items that round a value 1/4 or more off its integer are "
+                                      "redone in the reference's expression trees inside the timed launches "
+                                      "(DESIGN.md §6.1)") if "fused" in kernels else
+                                     "reference expression trees throughout (no guard, no admission assumption)"},
             "kernel_build_id": kernel_build_id(),
             "kernel_source_sha256": kernel_source_hash(),
             "decrypt_check": all_correct,

@@ -46,8 +46,11 @@ def test_library_is_not_an_ab_build():
     src += open(os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_device.hpp")).read()
     src += open(os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_kernels_whole.hip")).read()
     assert "TFHE_KO_" not in src
-    # the only conditionals left: phase timing (itself an A/B build) and the build tag
-    assert set(re.findall(r"^#\s*if(?:n?def)?\s+(\w+)", src, flags=re.M)) == {"TFHE_PHASE_PROF", "TFHE_AB_BUILD"}
+    # the only conditionals left: phase timing (itself an A/B build), the build tag, and the
+    # 1/8 margin guard of round 6's A/B measurement (#error outside an A/B build)
+    assert set(re.findall(r"^#\s*if(?:n?def)?\s+(\w+)", src, flags=re.M)) == {"TFHE_PHASE_PROF", "TFHE_AB_BUILD",
+                                                                                "TFHE_GUARD_EIGHTH"}
+    assert '#error "TFHE_GUARD_EIGHTH is an A/B-build switch' in src
     assert sum(1 for _ in open(os.path.join(ROOT, "zig-tfhe_amd", "csrc", "tfhe_kernels.hip"))) <= 3000
 
 

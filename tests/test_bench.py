@@ -81,7 +81,7 @@ def test_clock_and_frac_at_clock_from_committed_pmc(monkeypatch):
     if "clock_ghz" not in pmc:
         pytest.skip("the committed PMC record predates the clock pass")
     monkeypatch.setattr(bench, "kernel_build_id", lambda: pmc["kernel_build_id"])
-    clk = pmc["raw_per_launch"]["GRBM_GUI_ACTIVE"] / 8 / pmc["clock_pass_kernel_ns"]
+    clk = pmc["grbm_gui_active_per_launch"] / 8 / pmc["clock_pass_kernel_ns"]
     assert pmc["clock_ghz"] == pytest.approx(clk, abs=1e-3)
     p = tfhe_amd.make_params("128")
     kernel_s = 5.97e-3

@@ -852,3 +852,40 @@ def test_fused_equals_reference_soak_all_gates(oracle, pname):
                 want[m] = TRUTH[o](a.astype(bool)[m], b.astype(bool)[m])
             assert np.array_equal(sk.decrypt_bool(fused), want)
     assert c.near_tie_items() - before <= 4
+
+
+def test_worst_admitted_key_under_the_product_guard(oracle):
+    """the worst admitted key tools/admission_search.py found
+    (tests/golden/admission_worst.npz; gap 0.125 between the fused and the reference
+    trees) on the GPU.  BK[0] holds its rows, the other steps zero; the test vector
+    makes step 0's tmp the digits sign-aligned with those rows at the searched
+    output (a~_0 = N: tmp = -2 acc; b~ = 2N), so step 0 is the largest external
+    product the key admits and the rest add exact zeros.  The key is admitted (the
+    default runs the fused arithmetic under the margin guard), and every word of the
+    GPU's blind rotation equals the oracle's reference trees."""
+    from test_oracle import _aligned_x
+    f = np.load(os.path.join(GOLDEN, "admission_worst.npz"))
+    p = get_keys(oracle, "128").p
+    rows = f["rows"].astype(np.int64)
+    x = _aligned_x(oracle, p, rows, int(f["k"]), int(f["part"])).astype(np.uint64)
+    tv = (((1 << 32) - x) % (1 << 32) // 2).astype(np.uint32)  # -2 tv == x (mod 2^32): x is even
+    assert np.array_equal((np.uint64(0) - 2 * tv.astype(np.uint64)) % (1 << 32), x)
+    bk = np.zeros((p.n, 2 * p.L, 2, p.N))
+    for i in range(2 * p.L):
+        for part in range(2):
+            bk[0, i, part] = oracle.ifft((rows[i][part] % (1 << 32)).astype(np.uint32))
+    off = oracle.decomposition_offset(p)
+    ksk = np.zeros((p.N * p.iks_t * (1 << p.basebit), p.n + 1), np.uint32)
+    g = rng(9191)
+    cts = g.integers(0, 1 << 32, (5, p.n + 1), dtype=np.uint64).astype(np.uint32)
+    cts[:, 0], cts[:, p.n] = 1 << 31, 0  # a~_0 = N, b~ = 2N
+    c = tfhe_amd.Context("128", 0)
+    try:
+        c.load_cloud_key(off, tv, bk, ksk)
+        assert c.get_option("fused_admitted") == 1
+        got = c.blind_rotate_batch(cts)
+        want = np.array([oracle.blind_rotate(p, ct, tv, bk, off) for ct in cts])
+        assert np.array_equal(got, want)
+        print(f"worst admitted key: {c.near_tie_items()} item(s) recomputed by the guard")
+    finally:
+        c.close()

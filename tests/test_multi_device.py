@@ -325,13 +325,13 @@ def test_lut_dev_refuses_multi_device_context(oracle):
 
 def test_host_staging_modes_same_words(oracle):
     """TFHE_OPT_HOST_STAGING (round 6): the host-buffer entries of an
-    8-shard context through pageable copies (0), per-device pinned staging (1) and the
-    default (2 = auto: pinned on a multi-device context) give the same words as one
-    device, on a ragged gate batch, a bootstrap batch and a blind rotation (TRLWE
-    outputs, the largest D2H); a single-device context stays pageable under auto."""
+    8-shard context through pageable copies (0, the default) and per-device pinned
+    staging (1) give the same words as one device, on a ragged gate batch, a bootstrap
+    batch and a blind rotation (TRLWE outputs, the largest D2H), the arena reused
+    across calls; staging forced on a single-device context too."""
     single, k = loaded(oracle, "80")
     multi, _ = loaded(oracle, "80", devices=[0] * 8)
-    assert multi.get_option("host_staging") == tfhe_amd.STAGING_AUTO
+    assert multi.get_option("host_staging") == tfhe_amd.STAGING_PAGEABLE
     g = rng(83)
     B = 1030
     ops = g.integers(0, 10, B).astype(np.uint8)
@@ -339,7 +339,7 @@ def test_host_staging_modes_same_words(oracle):
     want = single.gate_batch(ops, A, Bc)
     want_bs = single.bootstrap_batch(A[:77])
     want_br = single.blind_rotate_batch(Bc[:40])
-    for mode in (tfhe_amd.STAGING_PAGEABLE, tfhe_amd.STAGING_PINNED, tfhe_amd.STAGING_AUTO):
+    for mode in (tfhe_amd.STAGING_PINNED, tfhe_amd.STAGING_PAGEABLE):
         with multi.options(host_staging=mode):
             for _ in range(2):  # the arena reused from offset 0 after each synchronisation
                 assert np.array_equal(multi.gate_batch(ops, A, Bc), want), mode

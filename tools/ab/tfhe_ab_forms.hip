@@ -885,6 +885,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide2(
     }
 }
 
+hipError_t ab_launch_wide_rc(const KParams &P, const DevTables &T, const uint8_t *ops, const uint32_t *in_a,
+                             const uint32_t *in_b, const uint32_t *idx, const uint32_t *testvec, const double2 *bk2,
+                             uint32_t *out, int out_mode, size_t B, hipStream_t s, const char **used);  // tfhe_kernels.hip
 hipError_t ab_launch_assist_dev(int var, dim3 grid, dim3 block, hipStream_t s, const KParams &P, const DevTables &T,
                                 const uint8_t *ops, const uint32_t *in_a, const uint32_t *in_b, const uint32_t *idx,
                                 const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B,
@@ -897,6 +900,10 @@ hipError_t ab_launch_blind_rotate(int br_form, const KParams &P, const DevTables
                                   const uint32_t *testvec, const double2 *bk2, uint32_t *out, int out_mode, size_t B,
                                   hipStream_t s, bool fused, const char **used) {
     const bool small = std::ldexp(2.0 * P.L * 1024.0, P.bgbit - 1 + 31) < std::ldexp(1.0, 49);
+    if (br_form == 30) {  // the latency form with row counters (tfhe_kernels.hip, RC = 1)
+        if (!(P.L == 3 && small && fused)) return hipErrorInvalidValue;
+        return ab_launch_wide_rc(P, T, ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B, s, used);
+    }
     if (br_form == 6) {  // duo: two computing waves per item
         const dim3 grid((unsigned)((B + BD_GATES - 1) / BD_GATES)), block(64 * BD_WAVES);
         if (P.L == 3 && small && fused) {

@@ -36,12 +36,14 @@ def clock_from_grbm(d, kernel):
         act = collections.defaultdict(float)
         for r in rows:
             act[r["Dispatch_Id"]] += float(r["Counter_Value"])
-        pairs = [(act[k], dur[k]) for k in act if k in dur and dur[k] > 0]
+        # warm launches only: the pass runs the batch several times, the first is cold
+        ids = sorted((k for k in act if k in dur and dur[k] > 0), key=int)
+        pairs = [(act[k], dur[k]) for k in (ids[1:] if len(ids) > 1 else ids)]
         if not pairs:
             continue
         a, ns = sum(p[0] for p in pairs), sum(p[1] for p in pairs)
         return {"clock_ghz": round(a / 8 / ns, 4), "grbm_gui_active_per_launch": a / len(pairs),
-                "clock_pass_kernel_ns": ns / len(pairs),
+                "clock_pass_kernel_ns": ns / len(pairs), "clock_pass_launches": len(pairs),
                 "clock_basis": "GRBM_GUI_ACTIVE / 8 XCDs / the dispatch's kernel-trace duration, in a profiled "
                                "pass of its own (profiled passes clock lower than unprofiled runs)"}
     return None

@@ -510,12 +510,32 @@ DEV uint32_t torus_from_f64_small(double v) {
 // launch (one v_bitop3 per two values); bit 0 clear sends the item to the
 // reference-tree recompute (near_tie_flag, k_blind_rotate FALLBACK), which
 // replaces every word of the item.
+// A/B build only (TFHE_GUARD_EIGHTH, round 6): the guard at 1/8.
+// s = v + (1.5*2^50 + 3/4) (|v| < 2^49) has mantissa 2^51 + Q, Q = rint(4v + 3):
+// Q mod 4 == 3 <=> |v - rint(v)| < 1/8, and then Q >> 2 (bits 33..2) is rint(v).  Same
+// instruction count; the margin to the reference becomes 3/8.  Not the product's: honest
+// rotations reach 1/8 about once per 10^10 values, i.e. a recompute
+// launch in a sizeable fraction of 1,024-gate batches.
+#ifdef TFHE_GUARD_EIGHTH
+#ifndef TFHE_AB_BUILD
+#error "TFHE_GUARD_EIGHTH is an A/B-build switch (Makefile EXTRA, tools/ab_forms.sh)"
+#endif
+constexpr uint32_t NEAR_MASK = 3u;
+DEV uint32_t torus_from_f64_guarded(double v, uint32_t &near) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v + 1688849860263936.75);
+    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    near &= lo;
+    return __builtin_amdgcn_alignbit(hi, lo, 2);
+}
+#else
+constexpr uint32_t NEAR_MASK = 1u;
 DEV uint32_t torus_from_f64_guarded(double v, uint32_t &near) {
     const uint64_t b = (uint64_t)__double_as_longlong(v + 3377699720527872.5);
     const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
     near &= lo;
     return __builtin_amdgcn_alignbit(hi, lo, 1);
 }
+#endif
 
 template <bool SMALL, bool FU = false>
 DEV uint32_t to_torus(double v, uint32_t &near) {
@@ -527,7 +547,7 @@ constexpr uint32_t NEAR_NONE = ~0u;
 // End of a fused item: if any lane of this wave rounded near a tie, flag item g
 // (one byte, a vector store; the flag is rare, the ballot is one SALU compare).
 DEV void near_tie_flag(const KParams &P, uint32_t near, size_t g, bool valid) {
-    if (__builtin_amdgcn_ballot_w64((near & 1u) == 0u) != 0 && valid && P.tie_flags && (threadIdx.x & 63) == 0)
+    if (__builtin_amdgcn_ballot_w64((near & NEAR_MASK) != NEAR_MASK) != 0 && valid && P.tie_flags && (threadIdx.x & 63) == 0)
         P.tie_flags[g] = 1;
 }
 

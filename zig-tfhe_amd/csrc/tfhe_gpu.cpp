@@ -151,8 +151,7 @@ struct tfhe_gpu_ctx {
     int64_t pipeline = 0;  // TFHE_OPT_HOST_PIPELINE (off by default: measured slower)
     // host-buffer copies through pinned staging (TFHE_OPT_HOST_STAGING; h2d / d2h_sync): the
     // arena's bytes in use since the last synchronisation of this context's stream
-    int64_t host_staging = TFHE_STAGING_AUTO;
-    bool in_multi = false;  // a device of a multi-device context (auto staging: pinned)
+    int64_t host_staging = TFHE_STAGING_PAGEABLE;
     char *stage_in = nullptr, *stage_out = nullptr;
     size_t stage_in_bytes = 0, stage_out_bytes = 0, stage_used = 0;
     std::vector<ncclComm_t> comms;   // one communicator per shard, created on the first key broadcast
@@ -328,9 +327,7 @@ int run_bootstrap_dev(tfhe_gpu_ctx *c, const uint8_t *ops, const uint32_t *a, co
     return TFHE_OK;
 }
 
-bool staged(const tfhe_gpu_ctx *c) {
-    return c->host_staging == TFHE_STAGING_PINNED || (c->host_staging == TFHE_STAGING_AUTO && c->in_multi);
-}
+bool staged(const tfhe_gpu_ctx *c) { return c->host_staging == TFHE_STAGING_PINNED; }
 
 // Pinned host buffer of at least `bytes` (grown by doubling; nothing may be in flight from it).
 int ensure_stage(tfhe_gpu_ctx *c, char *&p, size_t &have, size_t bytes) {
@@ -347,7 +344,8 @@ int ensure_stage(tfhe_gpu_ctx *c, char *&p, size_t &have, size_t bytes) {
 // Host -> device into `buf`.  Pageable: one hipMemcpyAsync from the caller's buffer.  Staged
 // (TFHE_OPT_HOST_STAGING): a host memcpy into this context's pinned arena, then the DMA from
 // there, so concurrent shards' copies do not go through the runtime's pageable staging
-// (measured serialised across host threads).  The arena is reused from
+// (for hosts where those serialise across host threads; on the MI355X box they do not and
+// pageable copies are faster).  The arena is reused from
 // offset 0 after every synchronisation of the stream (d2h_sync); when it is full the stream
 // is synchronised first, so no copy in flight ever reads overwritten bytes.
 int h2d(tfhe_gpu_ctx *c, DevBuf &buf, const void *src, size_t bytes) {
@@ -1878,7 +1876,7 @@ bool option_ok(const tfhe_gpu_ctx *c, int key, int64_t v, std::string &why) {
     case TFHE_OPT_BR_SPIN_CAP: ok = v >= 0 && v <= 0xFFFFFFFFll; break;
     case TFHE_OPT_HOST_PIPELINE: ok = v == 0 || v == 1; break;
     case TFHE_OPT_CIRCUIT_SPLIT: ok = v >= 0 && v <= 2; break;
-    case TFHE_OPT_HOST_STAGING: ok = v == TFHE_STAGING_PAGEABLE || v == TFHE_STAGING_PINNED || v == TFHE_STAGING_AUTO; break;
+    case TFHE_OPT_HOST_STAGING: ok = v == TFHE_STAGING_PAGEABLE || v == TFHE_STAGING_PINNED; break;
     case TFHE_OPT_TWIDDLES:
         ok = v == TFHE_TWIDDLES_GLIBC || v == TFHE_TWIDDLES_FDLIBM;
         // tfhe_gpu_keygen transformed the resident BK with the current tables:
@@ -2432,8 +2430,6 @@ int tfhe_gpu_create_multi(const tfhe_params *params, int num_devices, const int 
         }
         root->shards.push_back(s);
     }
-    if (num_devices > 1)
-        for (tfhe_gpu_ctx *s : root->shards) s->in_multi = true;  // auto host staging: pinned
     std::vector<int> sorted = devs;
     std::sort(sorted.begin(), sorted.end());
     root->distinct_devices = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();

@@ -284,7 +284,15 @@ constexpr size_t BR_WIDE_MAX_ITEMS = 512;  // measured: 1 gate 4.3 vs 9.9 ms; 51
 constexpr int WIDE_INV_W0 = 2;
 constexpr int WIDE_ROW45_PRIO = 1;
 
-template <int L, bool SMALL, bool FU = false>
+// RC (row counters, round 6; L = 3): no workgroup barrier between the
+// forward and inverse phases.  Each row wave publishes its two term spectra with a per-row LDS
+// counter; the inverse waves (2, 3) sum their output's six rows themselves, in the reference's
+// row order, each row as soon as its counter says it landed, so most of the sum runs while the
+// last rows are still transforming, and the sums stay in registers for the inverse.  Rows 0, 1
+// move to waves 2, 3 (the SIMDs that carry one row wave each: the first rows of the order land
+// first), rows 2, 3 to waves 0, 1 at issue priority 1 over rows 4, 5 on their shared SIMDs.
+// Same row order and arithmetic: the same words.
+template <int L, bool SMALL, bool FU = false, int RC = 0>
 __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     KParams P, DevTables TT, const uint8_t *__restrict__ ops, const uint32_t *__restrict__ in_a,
     const uint32_t *__restrict__ in_b, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ testvec,
@@ -297,6 +305,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     __shared__ __attribute__((aligned(16))) uint32_t s_acc[2048];
     __shared__ uint16_t s_at[1024];
     __shared__ int s_bt;
+    __shared__ uint32_t s_rows[8];  // RC: terms of row r published for steps < s_rows[r]
+    static_assert(!RC || L == 3, "row counters: L = 3");
     const int tid = threadIdx.x;
     const int t = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -310,6 +320,9 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
 
     for (int x = tid; x < 511; x += 512) s_tw[x] = TT.tw[x];
     for (int x = tid; x < 512; x += 512) s_twist[x] = TT.twist[x];
+    if (RC && tid < 8) s_rows[tid] = 0u;
+    // the row this wave transforms (RC: rows 0, 1 on waves 2, 3; rows 2, 3 on waves 0, 1)
+    const int row = RC && w < 4 ? w ^ 2 : w;
     if (w == 0) {
         for (int i = t; i <= n; i += 64) {
             uint32_t c = gate_combine(op, A[i], Bv[i], i == n);
@@ -324,7 +337,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
 #pragma unroll
         for (int q = 0; q < 8; q++)
 #pragma unroll
-            for (int h = 0; h < 2; h++) kr[q][h] = bkd[((size_t)w * 8 + q) * 128 + h * 64 + t];
+            for (int h = 0; h < 2; h++) kr[q][h] = bkd[((size_t)row * 8 + q) * 128 + h * 64 + t];
     }
     __syncthreads();
     const int bt = __builtin_amdgcn_readfirstlane(s_bt);
@@ -343,8 +356,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     const int ipoly = w - WIDE_INV_W0;
     const bool is_inv = ipoly == 0 || ipoly == 1;
     // row waves that issue their BK prefetch in the inverse phase (the others
-    // right after their terms)
-    const bool pf_late = w < 2 * L && !is_inv;
+    // right after their terms; RC: every row wave right after its terms)
+    const bool pf_late = !RC && w < 2 * L && !is_inv;
     // the inverse waves keep their polynomial's 16 accumulator words per lane
     // in registers: the update then waits for no LDS read
     uint32_t accr[16];
@@ -355,7 +368,10 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
 
     // rows 4 and 5 share their SIMDs with rows 0 and 1 and finish the forward
     // phase last; at a higher issue priority they take the VALU first
-    if (w == 4 || w == 5) __builtin_amdgcn_s_setprio(WIDE_ROW45_PRIO);
+    // (RC: rows 2 and 3 on waves 0 and 1 instead, ahead of rows 4 and 5 in the sum's order)
+    if (RC ? (w == 0 || w == 1) : (w == 4 || w == 5)) __builtin_amdgcn_s_setprio(WIDE_ROW45_PRIO);
+    uint32_t fail = 0;  // RC: a row-counter wait gave up (report_wait_failure)
+    const uint32_t spin_cap = P.spin_cap ? P.spin_cap : BR_SPIN_CAP_DEFAULT;
     int at_next = s_at[0];  // a~ read one step ahead (its wait would drain every LDS op)
     uint32_t near = NEAR_NONE;  // FU: margin guard (the inverse waves)
     PhaseProf pp;  // development timing (TFHE_PHASE_PROF), per wave
@@ -365,8 +381,8 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
         const int at = __builtin_amdgcn_readfirstlane(at_next);
         at_next = s_at[i + 1 < n ? i + 1 : i];
         if (w < 2 * L) {
-            const int poly = w >= L ? 1 : 0;
-            const int level = w - poly * L;
+            const int poly = row >= L ? 1 : 0;
+            const int level = row - poly * L;
             const uint32_t *pa = s_acc + poly * 1024;
             // gathers and own words first, arithmetic after (one wait)
             uint32_t rot[16], own[16];
@@ -391,14 +407,18 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
                                        twist_t[64 * m]);
             }
             pp.mark(10);
-            fft512<1, false, FU>(d, s_prod[0][w], T, t);
+            fft512<1, false, FU>(d, s_prod[0][row], T, t);
             pp.mark(11);
             // this row's terms of fmaInFd1024 for both outputs, every frequency
-            // (after this wave's exchanges in s_prod[0][w])
+            // (after this wave's exchanges in s_prod[0][row])
 #pragma unroll
             for (int q = 0; q < 8; q++) {
-                s_prod[0][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][0]);
-                s_prod[1][w][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][1]);
+                s_prod[0][row][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][0]);
+                s_prod[1][row][t + 64 * q] = cmul_bk<FU>(d[0][q], kr[q][1]);
+            }
+            if (RC) {
+                __builtin_amdgcn_sched_barrier(0);
+                counter_add(s_rows + row);  // the terms land before the count (one wave's LDS ops run in order)
             }
             pp.mark(14);
             // next step's BK row, landing under the sum, inverse and forward
@@ -409,7 +429,52 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
             // critical path (rows 4 and 5 share SIMDs with rows 0 and 1):
             // 104.7 -> 101.8 ms per 16-bit adder with the inverse on waves 2, 3
             // (profiles/r03q_wide_prefetch_inverse.txt).
-            if (i + 1 < n && !pf_late) wide_prefetch(kr, bkd + (size_t)(i + 1) * trgsw, w, t);
+            if (i + 1 < n && !pf_late) wide_prefetch(kr, bkd + (size_t)(i + 1) * trgsw, row, t);
+        }
+        if (RC) {
+            if (is_inv) {
+                // this output's sum over rows 0..2L-1 in the reference's order, each row once
+                // its counter shows this step's terms (fmaInFd1024 starts from 0.0: 0.0 + x == x)
+                C2 fs[8];
+                pp.mark(2);
+#pragma unroll
+                for (int r = 0; r < 2 * L; r++) {
+                    uint32_t f = 0;
+                    spin_until_ge<1>(s_rows + r, (uint32_t)i + 1u, spin_cap, f);
+                    fail |= f;
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const C2 tq = s_prod[ipoly][r][t + 64 * q];
+                        fs[q] = r == 0 ? tq : c2(fs[q].x + tq.x, fs[q].y + tq.y);
+                    }
+                }
+                pp.mark(4);
+                C2 e[1][8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) e[0][q] = fs[br3(q)];
+                C2 twr[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) twr[q] = twist_t[64 * q];
+                pp.mark(12);
+                // exchange buffer: row 0's term spectrum of this output, already summed; only
+                // this wave reads it this step, and row 0's wave rewrites it after the barrier
+                fft512<1, true, FU>(e, s_prod[ipoly][0], T, t);
+                pp.mark(13);
+                uint32_t *pa = s_acc + ipoly * 1024;
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    double re, im;
+                    untwist_out<false, FU>(e[0][q], twr[q], re, im);
+                    accr[q] += to_torus<SMALL, FU>(re, near);
+                    accr[q + 8] += to_torus<SMALL, FU>(im, near);
+                    pa[t + 64 * q] = accr[q];
+                    pa[t + 64 * q + 512] = accr[q + 8];
+                }
+            }
+            pp.mark(5);
+            __syncthreads();  // accumulator updated, every term read
+            continue;
         }
         pp.mark(1);
         __syncthreads();  // every row's terms are in place
@@ -429,7 +494,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
         pp.mark(3);
         __syncthreads();  // both product spectra complete
         pp.mark(4);
-        if (pf_late && i + 1 < n) wide_prefetch(kr, bkd + (size_t)(i + 1) * trgsw, w, t);
+        if (pf_late && i + 1 < n) wide_prefetch(kr, bkd + (size_t)(i + 1) * trgsw, row, t);
         if (is_inv) {
             C2 e[1][8];
 #pragma unroll
@@ -459,6 +524,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     if (t == 0)
         for (int k = 0; k < 16; k++) atomicAdd(&g_phase_cycles[w * 16 + k], (unsigned long long)pp.acc[k]);
 #endif
+    if (RC) report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU) near_tie_flag(P, near, g, true);
 
     if (w != 0) return;
@@ -1395,6 +1461,20 @@ static hipError_t launch_blind_rotate_form(const KParams &P, const DevTables &T,
 #undef BR_LAUNCH
     return hipGetLastError();
 }
+
+#ifdef TFHE_AB_BUILD
+// A/B builds only (tools/ab/tfhe_ab_forms.hip, TFHE_OPT_BR_FORM 30): the latency form with row
+// counters (RC = 1) at L = 3, fused.
+hipError_t ab_launch_wide_rc(const KParams &P, const DevTables &T, const uint8_t *ops, const uint32_t *in_a,
+                             const uint32_t *in_b, const uint32_t *idx, const uint32_t *testvec, const double2 *bk2,
+                             uint32_t *out, int out_mode, size_t B, hipStream_t s, const char **used) {
+    if (P.L != 3) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_blind_rotate_wide<3, true, true, 1>), dim3((unsigned)B), dim3(64 * BW_WAVES), 0, s, P, T,
+                       ops, in_a, in_b, idx, testvec, bk2, out, out_mode, B);
+    if (used) *used = "k_blind_rotate_wide<3,true,true,RC> (latency form, row counters, fused)";
+    return hipGetLastError();
+}
+#endif
 
 // Modelled blind-rotation time on a device with `cus` CUs, in whole-form
 // rounds (BR_WAVES x cus items), of the launch plans launch_blind_rotate picks

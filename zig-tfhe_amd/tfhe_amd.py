@@ -28,7 +28,7 @@ OPTIONS = {"br_form": 1, "br_loader": 2, "ks_form": 3, "ks_narrow": 4, "ks_item_
 READONLY_OPTIONS = {"fused_admitted": 14, "level_issue_us": 15, "key_row_rms_ppm": 16}  # tfhe_gpu_get_option only
 OPTION_DEFAULTS = {"br_form": 0, "br_loader": 1, "ks_form": 3, "ks_narrow": 0, "ks_item_groups": 0,
                    "ks_sel_items": 8, "circuit_pack": 1, "twiddles": 0, "arith": 0, "br_sync": 1, "br_spin_cap": 0,
-                   "host_pipeline": 0, "circuit_split": 0, "host_staging": 2}
+                   "host_pipeline": 0, "circuit_split": 0, "host_staging": 0}
 # status codes (include/tfhe_gpu.h TFHE_ERR_*)
 ERR_INVALID, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_IO, ERR_DEVICE = -1, -2, -3, -4, -5, -6
 # 2 split, 4 pair: removed (round 4); 6 duo, 7 wide2: A/B libraries only (tools/ab/, round 5); 5 octo: L = 1
@@ -36,7 +36,7 @@ BR_FORMS = {"auto": 0, "whole": 1, "wide": 3, "octo": 5, "duo": 6, "wide2": 7, "
 BUILD_PRODUCT, BUILD_AB = 0, 1  # tfhe_gpu_build_kind
 TWIDDLES_GLIBC, TWIDDLES_FDLIBM = 0, 1
 ARITH_AUTO, ARITH_REFERENCE, ARITH_FUSED_FORCED = 0, 1, 2
-STAGING_PAGEABLE, STAGING_PINNED, STAGING_AUTO = 0, 1, 2  # TFHE_OPT_HOST_STAGING
+STAGING_PAGEABLE, STAGING_PINNED = 0, 1  # TFHE_OPT_HOST_STAGING
 
 # gate op codes, include/tfhe_gpu.h TFHE_GATE_* (gates.zig:48-121)
 NAND, OR, AND, XOR, XNOR, NOR, ANDNY, ANDYN, ORNY, ORYN = range(10)
@@ -276,7 +276,7 @@ class Context:
     def set_option(self, name: str, value: int):
         """tfhe_gpu_set_option (kernel forms, twiddle source; OPTIONS)."""
         if name == "br_form" and isinstance(value, str):
-            value = BR_FORMS[value]
+            value = int(value) if value.isdigit() else BR_FORMS[value]
         key = READONLY_OPTIONS[name] if name in READONLY_OPTIONS else OPTIONS[name]  # read-only: the library refuses
         self.check(self.lib.tfhe_gpu_set_option(self.h, key, int(value)), f"set_option({name})")
 
