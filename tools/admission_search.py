@@ -42,9 +42,12 @@ MODES = (1, 4, 3)
 PRODUCT_MODES = (1, 4)  # the product's fused forms; mode 3 (regrouped sums) is the A/B-only duo form
 
 
-def _setup():
+PARAMS = "128"  # --params: the set whose decomposition (offset, L, Bg) the external product uses
+
+
+def _setup(pname=None):
     from oracle import Oracle, params
-    return Oracle(), params("128")
+    return Oracle(), params(pname or PARAMS)
 
 
 def spectrum_max(o, rows):
@@ -120,8 +123,8 @@ def start_rows(kind, g):
 
 
 def worker(args):
-    kind, seed, iters, rms_cap, target = args
-    o, p = _setup()
+    kind, seed, iters, rms_cap, target, pname = args
+    o, p = _setup(pname)
     g = np.random.default_rng(seed)
     rows = start_rows(kind, g)
     while not admitted(o, rows, rms_cap):  # scale a start point in under the caps
@@ -170,19 +173,21 @@ def main():
     ap.add_argument("--rms-cap", type=float, default=0.70,
                     help="largest admitted row RMS / 2^31 (0: the spectrum cap alone, round 4's rule)")
     ap.add_argument("--target", default="", help="comma-separated modes the hill climb maximises (default: all)")
+    ap.add_argument("--params", default="128", choices=["128", "80"],
+                    help="parameter set (80-bit: the same L = 3, Bg = 2^6, N = 1024 external product, params.zig:70-95)")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05_admission_search.json"))
     ap.add_argument("--fixture", default=os.path.join(ROOT, "tests", "golden", "admission_worst.npz"))
     a = ap.parse_args()
     kinds = ("max_magnitude", "keygen_like", "low_frequency_scaled", "sparse_max")
     target = tuple(int(m) for m in a.target.split(",")) if a.target else None
-    jobs = [(kinds[r % len(kinds)], 5000 + r, a.iters, a.rms_cap, target) for r in range(a.restarts)]
+    jobs = [(kinds[r % len(kinds)], 5000 + r, a.iters, a.rms_cap, target, a.params) for r in range(a.restarts)]
     t0 = time.time()
     with mp.get_context("spawn").Pool(a.workers) as pool:
         res = pool.map(worker, jobs)
     worst = max(res, key=lambda r: max(r["max_gap_per_mode"][str(m)] for m in PRODUCT_MODES))
     per_mode = {str(m): max(r["max_gap_per_mode"][str(m)] for r in res) for m in MODES}
     rec = {"method": __doc__.split("\n\n")[0].replace("\n", " "),
-           "restarts": a.restarts, "iters_per_restart": a.iters, "cap_log2": 39, "row_rms_cap": a.rms_cap,
+           "params": a.params, "restarts": a.restarts, "iters_per_restart": a.iters, "cap_log2": 39, "row_rms_cap": a.rms_cap,
            "objective_modes": list(target or MODES),
            "modes": {"1": "fused trees (whole, octo, latency forms' forward/MAC order)", "4": "latency form's summed row terms",
                      "3": "regrouped sums (duo form, A/B libraries only)"},
@@ -195,7 +200,8 @@ def main():
            "runs": [{k: r[k] for k in ("kind", "seed", "start", "best", "max_gap_per_mode", "spectrum_max_log2",
                                        "row_rms_max", "all_flagged")} for r in res]}
     json.dump(rec, open(a.out, "w"), indent=1)
-    np.savez_compressed(a.fixture, rows=worst["rows"], k=worst["k"], part=worst["part"], gap=worst["best"])
+    if a.fixture:  # --fixture '': no fixture written
+        np.savez_compressed(a.fixture, rows=worst["rows"], k=worst["k"], part=worst["part"], gap=worst["best"])
     print(json.dumps({k: rec[k] for k in ("max_gap_per_mode", "max_gap_product", "worst", "every_parting_word_flagged",
                                           "seconds")}, indent=1))
 

@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 using namespace tfhe;
@@ -55,7 +56,11 @@ int main(int argc, char **argv) {
         O.br_form = form[0] == 'w' && form[1] == 'i' ? 3 : 1;
         const bool assist = O.br_form == 1;  // L = 3 fused: the whole form with loader assist
         const bool dev = form[0] == 'd';
-        if (dev)
+        const bool rc = std::string(form) == "widerc";  // the latency form with row counters (A/B form 30)
+        if (rc)
+            CK(ab_launch_wide_rc(P, T, nullptr, d_in, nullptr, nullptr, d_tv, (const double2 *)d_bk, d_out, BR_OUT_LV1, B,
+                                 0, nullptr));
+        else if (dev)
             CK(ab_launch_assist_dev(atoi(form + 3), dim3((unsigned)((B + 3) / 4)), dim3(512), 0, P, T, nullptr, d_in,
                                     nullptr, nullptr, d_tv, (const double2 *)d_bk, d_out, BR_OUT_LV1, B, nullptr));
         else
@@ -68,8 +73,11 @@ int main(int argc, char **argv) {
         CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
 #endif
         if (O.br_form == 3) {  // latency form: per wave, per phase (ticks per step per gate)
-            const char *wn[16] = {"fwd(other)", "barrier1", "sum", "barrier2", "inverse(other)", "barrier3", "tail", "-",
-                                  "row: gather", "row: digits+twist", "row: fft", "row: terms", "inv: fft", "inv: untwist+add", "row: prefetch issue", "-"};
+            const char *wn0[16] = {"fwd(other)", "barrier1", "sum", "barrier2", "inverse(other)", "barrier3", "tail", "-",
+                                   "row: gather", "row: digits+twist", "row: fft", "row: terms", "inv: fft", "inv: untwist+add", "row: prefetch issue", "-"};
+            const char *wnrc[16] = {"fwd(other)", "-", "inv: row waits+sum", "-", "inv: operands", "barrier", "tail", "-",
+                                    "row: gather", "row: digits+twist", "row: fft", "row: terms+count", "inv: fft", "inv: untwist+add", "row: prefetch, wait", "-"};
+            const char **wn = rc ? wnrc : wn0;
             printf("rep %d: %.3f ms (%zu gates); s_memtime ticks per step, per wave:\n", rep, ms, B);
             for (int k = 0; k < 16; k++) {
                 if (k == 6 || k == 7 || k > 14) continue;
