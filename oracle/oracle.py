@@ -26,7 +26,7 @@ class OracleParams(C.Structure):
 # Parameter sets, params.zig.  KSK/BSK alphas: the reference hard-wires the
 # 128-bit constants (params.zig:419-422) for every set; UINT4 keeps its own
 # lv0/KSK noise and a zero BSK noise (its 2^-52 alpha is below the torus
-# resolution; DESIGN.md §Parameters).
+# resolution; DESIGN.md §6.3).
 PARAM_SETS = {
     "128": dict(n=700, N=1024, nbit=10, L=3, bgbit=6, basebit=2, iks_t=9,
                 alpha_lv0=2.0e-5, alpha_lv1=2.0e-8, alpha_ksk=2.0e-5, alpha_bsk=2.0e-8),   # :350-375

@@ -14,7 +14,7 @@
  * tolerance vs the naive product, gate truth tables, 402+304=706), see
  * tests/test_oracle.py.  Bit patterns of the f64 FFT path are therefore pinned
  * to this restatement + glibc 2.35 twiddles, "parity unpinned" vs the Zig
- * binary itself (DESIGN.md §Parity).
+ * binary itself (DESIGN.md §6).
  */
 #ifndef TFHE_ORACLE_H
 #define TFHE_ORACLE_H

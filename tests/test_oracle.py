@@ -700,7 +700,7 @@ def test_identity_key_switching(oracle, keys128):  # trgsw.zig:729-755
 # a.subMul(b, 2) + f64ToTorus(-0.25) = a - 2b - 1/4, which decrypts to
 # XOR(a, b), not XNOR (XOR uses a + 2b + 1/4).  The reference has no XNOR
 # truth-table test (its tests cover NAND/AND/OR/XOR/NOR/MUX), so the defect is
-# latent there; a drop-in must reproduce it bit for bit (DESIGN.md §Parity).
+# latent there; a drop-in must reproduce it bit for bit (DESIGN.md §6).
 TRUTH = {0: lambda a, b: not (a and b), 1: lambda a, b: a or b, 2: lambda a, b: a and b,
          3: lambda a, b: a != b, 4: lambda a, b: a != b, 5: lambda a, b: not (a or b),
          6: lambda a, b: (not a) and b, 7: lambda a, b: a and not b, 8: lambda a, b: (not a) or b,

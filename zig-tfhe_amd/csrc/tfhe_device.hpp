@@ -29,7 +29,7 @@
 // FFT mapping: one wavefront owns one 512-point complex transform (N=1024
 // negacyclic), 8 complex values per lane, three radix-2^3 register passes
 // (each pass = three radix-2 DIT stages with the reference's butterflies and
-// recurrence twiddles) and two conflict-free LDS exchanges (DESIGN.md §FFT).
+// recurrence twiddles) and two conflict-free LDS exchanges (DESIGN.md §4.1).
 // Lane t always owns coefficients / frequencies {t + 64q}, so the forward
 // output feeds the MAC and the inverse input with no data movement, and the
 // accumulator update is lane-local.
@@ -259,7 +259,7 @@ DEV void passBC(C2 *d, const C2 *w) {
 
 // Exchange 1 (after pass A): lane t wrote positions 8*br6(t)+q, reads
 // (t&7) + 8q + 64(t>>3).  XOR swizzle of the 16-B slot makes both the
-// ds_write_b128 and the ds_read_b128 bank-conflict-free (DESIGN.md §FFT).
+// ds_write_b128 and the ds_read_b128 bank-conflict-free (DESIGN.md §4.1).
 DEV int swz1(int p) {
     return p ^ ((((p >> 6) & 1) * 1) ^ (((p >> 7) & 1) * 10) ^ (((p >> 8) & 1) * 4));
 }

@@ -27,7 +27,7 @@
 // FFT mapping: one wavefront owns one 512-point complex transform (N=1024
 // negacyclic), 8 complex values per lane, three radix-2^3 register passes
 // (each pass = three radix-2 DIT stages with the reference's butterflies and
-// recurrence twiddles) and two conflict-free LDS exchanges (DESIGN.md §FFT).
+// recurrence twiddles) and two conflict-free LDS exchanges (DESIGN.md §4.1).
 // Lane t always owns coefficients / frequencies {t + 64q}, so the forward
 // output feeds the MAC and the inverse input with no data movement, and the
 // accumulator update is lane-local.

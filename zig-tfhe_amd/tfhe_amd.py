@@ -59,7 +59,7 @@ class TfheParams(C.Structure):
 
 # params.zig parameter sets (runtime form).  KSK/BSK noise: the reference's
 # KSK_ALPHA/BSK_ALPHA (params.zig:419-422) are the 128-bit constants; UINT4
-# keeps its own set's alphas (DESIGN.md §Parameters).
+# keeps its own set's alphas (DESIGN.md §6.3).
 SECURITY_128_BIT = dict(n=700, N=1024, nbit=10, L=3, bgbit=6, basebit=2, iks_t=9,
                         alpha_lv0=2.0e-5, alpha_lv1=2.0e-8, alpha_ksk=2.0e-5, alpha_bsk=2.0e-8)
 SECURITY_80_BIT = dict(n=550, N=1024, nbit=10, L=3, bgbit=6, basebit=2, iks_t=7,
@@ -70,7 +70,7 @@ SECURITY_UINT4 = dict(n=820, N=1024, nbit=10, L=1, bgbit=22, basebit=5, iks_t=3,
                       alpha_ksk=0.00000251676160959795544987084234,
                       # 2^-52 is below the 32-bit torus resolution; the reference's
                       # f64ToTorus would turn it into a {0,-1} bias that the
-                      # L=1/Bg=2^22 gadget amplifies 2^21x (DESIGN.md §Parameters)
+                      # L=1/Bg=2^22 gadget amplifies 2^21x (DESIGN.md §6.3)
                       alpha_bsk=0.0)
 PARAM_SETS = {"128": SECURITY_128_BIT, "80": SECURITY_80_BIT, "uint4": SECURITY_UINT4}
 
