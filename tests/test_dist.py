@@ -164,16 +164,21 @@ def test_gloo_key_broadcast_and_sharded_batch(world):
 
 
 @pytest.mark.gpu
-def test_key_blob_roundtrip_through_broadcast(oracle):
-    """export (ctx 0) -> torch.distributed.broadcast (world 1, gloo, device
-    tensors) -> import (ctx 1); gates through ctx 1 equal the oracle's."""
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_key_blob_roundtrip_through_broadcast(oracle, backend):
+    """export (ctx 0) -> torch.distributed.broadcast (world 1, device tensors) ->
+    import (ctx 1); gates through ctx 1 equal the oracle's.  The nccl case runs
+    the bench's multi-rank key path through RCCL itself (one rank: the box has one
+    GPU), fingerprint all-gather included."""
     import tfhe_amd
     from conftest import get_keys
 
     k = get_keys(oracle, "80")
     port = _free_port()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=0, world_size=1)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=0, world_size=1)
     try:
         dev = torch.device("cuda", 0)
         c0 = tfhe_amd.Context("80", 0)
