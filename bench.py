@@ -49,6 +49,9 @@ PMC_PATH = os.path.join(ROOT, "profiles", "pmc_blind_rotate.json")
 # rocprofv3 --kernel-trace --stats average of the blind-rotation kernel for the kernel
 # binary it was measured on (tools/rocprof_record.py writes it from a committed stats csv)
 ROCPROF_PATH = os.path.join(ROOT, "profiles", "rocprof_blind_rotate.json")
+# the blind rotation's core-clock cycles per launch (tools/bin/clock_probe: s_memtime over
+# s_memrealtime per wave, no phase marks; tools/clock_probe_record.py), invariant to DVFS
+CLOCK_PROBE_PATH = os.path.join(ROOT, "profiles", "clock_probe.json")
 REFERENCE_MS_PER_GATE = 37.31  # zig-tfhe's published single-thread gate time (CHANGELOG.md:86)
 
 
@@ -190,6 +193,16 @@ def pmc_record(batch: int, params: str):
     return pmc, None
 
 
+def clock_probe_record(batch: int, params: str):
+    """profiles/clock_probe.json if it was measured on this kernel binary's source, batch and params."""
+    if not os.path.exists(CLOCK_PROBE_PATH):
+        return None
+    rec = json.load(open(CLOCK_PROBE_PATH))
+    if rec.get("kernel_build_id") != kernel_build_id() or rec.get("batch") != batch or rec.get("params") != params:
+        return None
+    return rec
+
+
 def rooflines(p, B, params, br_avg_s, kernel):
     """Primary roofline: f64 VALU issue, the bound the blind rotation is on (its
     HBM traffic is ~60 GB/s): the kernel's f64 VALU lane-operations (model
@@ -214,13 +227,27 @@ def rooflines(p, B, params, br_avg_s, kernel):
                                      "frac": round(f64_ops_per_cmux(p.L) * p.n * B / br_avg_s / VALU_F64_PEAK, 4)},
             "arithmetic": "fused multiply-add (exact-integer regime, DESIGN.md §6)" if fused else "reference expression trees",
             "reference_tree_f64_ops_per_cmux": f64_ops_per_cmux(p.L)}
+    # the clock THIS run held: the kernel's core-clock cycles per launch (clock probe; the same at every
+    # clock) over this run's kernel time, and the fraction of the f64 issue peak AT that
+    # clock: how much of the gap to `frac` is DVFS
+    probe = clock_probe_record(B, params)
+    if probe:
+        clk = probe["cycles_per_launch"] / (br_avg_s * 1e9)
+        roof["clock_ghz"] = round(clk, 4)
+        roof["clock_provenance"] = (f"{probe['cycles_per_launch']:,} core-clock cycles per launch (+/- "
+                                    f"{probe['cycles_per_launch_spread']:,}) from committed record "
+                                    f"{os.path.relpath(CLOCK_PROBE_PATH, ROOT)} (kernel build id "
+                                    f"{probe['kernel_build_id']}), over this run's kernel time (HIP events)")
+        roof["frac_at_clock"] = round(f64_rate / (VALU_F64_PEAK / 2.4 * clk), 4)
     if pmc:
-        # the effective clock of the PMC's own clock pass (GRBM_GUI_ACTIVE / 8 / duration), and the
-        # fraction of the f64 issue peak AT that clock: how much of the gap to `frac` is DVFS
         if pmc.get("clock_ghz"):
-            roof["clock_ghz"] = pmc["clock_ghz"]
-            roof["clock_provenance"] = record_provenance(PMC_PATH, pmc) + "; " + pmc.get("clock_basis", "")
-            roof["frac_at_clock"] = round(f64_rate / (VALU_F64_PEAK / 2.4 * pmc["clock_ghz"]), 4)
+            # the PMC pass's own clock (GRBM_GUI_ACTIVE / 8 / duration): profiled passes run slower and clock
+            # lower; the line's clock when no clock-probe record matches
+            key = "clock_ghz_pmc_pass" if probe else "clock_ghz"
+            roof[key] = pmc["clock_ghz"]
+            if not probe:
+                roof["clock_provenance"] = record_provenance(PMC_PATH, pmc) + "; " + pmc.get("clock_basis", "")
+                roof["frac_at_clock"] = round(f64_rate / (VALU_F64_PEAK / 2.4 * pmc["clock_ghz"]), 4)
         roof["pmc"] = {k: pmc[k] for k in ("valu_f64_insts_per_launch", "valu_insts_per_item_per_cmux",
                                            "lds_insts_per_item_per_cmux", "valu_insts_per_gate_wave_per_cmux",
                                            "lds_insts_per_gate_wave_per_cmux", "wait_any_frac_all_waves")

@@ -74,19 +74,41 @@ def test_roofline_from_committed_records(monkeypatch):
     assert key["key_bytes_consumed_per_launch"] == bench.algorithmic_bytes_per_gate(p) * 1024
 
 
-def test_clock_and_frac_at_clock_from_committed_pmc(monkeypatch):
-    """roofline.clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / the clock pass's kernel duration, and
-    frac_at_clock = achieved / (1,024 SIMDs x 16 lanes x clock), both from the committed PMC file."""
+def test_clock_and_frac_at_clock_from_committed_records(monkeypatch):
+    """roofline.clock_ghz = the clock probe's cycles per launch / this run's kernel time, and
+    frac_at_clock = achieved / (1,024 SIMDs x 16 lanes x clock); the PMC pass's own clock
+    (GRBM_GUI_ACTIVE / 8 XCDs / its kernel duration) beside it."""
     pmc = json.load(open(bench.PMC_PATH))
-    if "clock_ghz" not in pmc:
-        pytest.skip("the committed PMC record predates the clock pass")
+    probe = json.load(open(bench.CLOCK_PROBE_PATH))
+    assert probe["kernel_build_id"] == pmc["kernel_build_id"]
     monkeypatch.setattr(bench, "kernel_build_id", lambda: pmc["kernel_build_id"])
-    clk = pmc["grbm_gui_active_per_launch"] / 8 / pmc["clock_pass_kernel_ns"]
-    assert pmc["clock_ghz"] == pytest.approx(clk, abs=1e-3)
+    # the record's cycle counts reproduce from its launches: event ms x GHz, after the clock ramp
+    settled = probe["launches"][3:]
+    assert probe["cycles_per_launch"] == pytest.approx(
+        sum(r["kernel_ms"] * r["clock_ghz"] for r in settled) / len(settled) * 1e6, rel=1e-4)
+    # and the wave span's count is the same at every clock the launches held (1.88-2.35 GHz)
+    spans = [r["wave_span_ms"] * r["clock_ghz"] * 1e6 for r in probe["launches"]]
+    assert max(spans) / min(spans) < 1.001 and min(r["clock_ghz"] for r in probe["launches"]) < 2.0
     p = tfhe_amd.make_params("128")
     kernel_s = 5.97e-3
     roof, _ = bench.rooflines(p, 1024, "128", kernel_s, "k_blind_rotate_assist<true> (whole form, fused)")
     ops = 145424 * 700 * 1024
-    assert roof["clock_ghz"] == pmc["clock_ghz"]
+    clk = probe["cycles_per_launch"] / (kernel_s * 1e9)
+    assert roof["clock_ghz"] == pytest.approx(clk, abs=1e-4)
     assert roof["frac_at_clock"] == pytest.approx(ops / kernel_s / (1024 * 16 * clk * 1e9), abs=1e-4)
     assert roof["frac_at_clock"] >= roof["frac"] - 1e-9 or clk > 2.4
+    assert "this run's kernel time" in roof["clock_provenance"]
+    # the PMC pass's clock, from its own counters
+    pclk = pmc["grbm_gui_active_per_launch"] / 8 / pmc["clock_pass_kernel_ns"]
+    assert pmc["clock_ghz"] == pytest.approx(pclk, abs=1e-3)
+    assert roof["clock_ghz_pmc_pass"] == pmc["clock_ghz"]
+
+
+def test_clock_falls_back_to_the_pmc_pass(monkeypatch, tmp_path):
+    """Without a matching clock-probe record the line states the PMC pass's clock, as in round 6's
+    first records."""
+    pmc = json.load(open(bench.PMC_PATH))
+    monkeypatch.setattr(bench, "kernel_build_id", lambda: pmc["kernel_build_id"])
+    monkeypatch.setattr(bench, "CLOCK_PROBE_PATH", str(tmp_path / "none.json"))
+    roof, _ = bench.rooflines(tfhe_amd.make_params("128"), 1024, "128", 5.97e-3, "k_blind_rotate_assist<true> (fused)")
+    assert roof["clock_ghz"] == pmc["clock_ghz"] and "clock_ghz_pmc_pass" not in roof

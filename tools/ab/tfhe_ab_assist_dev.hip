@@ -318,7 +318,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
         lp.mark(5);
 #ifdef TFHE_PHASE_PROF
         if (t == 0)
-            for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[16 + q], (unsigned long long)lp.acc[q]);
+            lp.flush(g_phase_cycles + 16, 8);
 #endif
         report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
         if (FU && VAR != 10) near_tie_flag(P, near, g, valid);  // VAR 10: garbage values
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist_dev(
     pp.mark(0);
 #ifdef TFHE_PHASE_PROF
     if (t == 0)
-        for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[q], (unsigned long long)pp.acc[q]);
+        pp.flush(g_phase_cycles, 8);
 #endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU && VAR != 10) near_tie_flag(P, near, g, valid);  // VAR 10: garbage values

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_duo(
     pp.mark(0);
 #ifdef TFHE_PHASE_PROF
     if (t == 0)
-        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], (unsigned long long)pp.acc[k]);
+        pp.flush(g_phase_cycles, 8);
 #endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU) near_tie_flag(P, near, g, valid);

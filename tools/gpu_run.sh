@@ -6,6 +6,7 @@
 #   tests     pytest -m gpu (whole suite)          smoke   __graft_entry__.smoke()
 #   prof      rocprofv3 --kernel-trace --stats of a 50-step bench -> rocprof record (warm-up
 #             excluded by position) + the blind-rotation PMC passes (with the GRBM clock pass)
+#   clock     tools/bin/clock_probe (core clock per wave, no phase marks) -> clock-probe record
 #   bench     the default bench line (CPU baseline included), with the records just measured
 #   bench2k   a 2,048-gate line                    arith1  the headline config under --opt arith=1
 #   copy      tools/bin/copy_bw (host copy rates, per-shard staging)
@@ -40,6 +41,10 @@ for S in ${STEPS//,/ }; do
     bash tools/pmc_br.sh $TAG.pmc 1024 "" gpurun_out/${TAG}_pmc_blind_rotate.json || exit 4
     cp gpurun_out/${TAG}_rocprof_blind_rotate.json profiles/rocprof_blind_rotate.json
     cp gpurun_out/${TAG}_pmc_blind_rotate.json profiles/pmc_blind_rotate.json ;;
+  clock)
+    timeout -k 10 120 tools/bin/clock_probe 1024 whole > gpurun_out/$TAG.clock_probe.txt 2>&1 || { tail gpurun_out/$TAG.clock_probe.txt; exit 1; }
+    python tools/clock_probe_record.py gpurun_out/$TAG.clock_probe.txt --out gpurun_out/${TAG}_clock_probe.json || exit 1
+    cp gpurun_out/${TAG}_clock_probe.json profiles/clock_probe.json ;;
   bench)
     timeout -k 10 600 python bench.py > gpurun_out/$TAG.bench.json 2> gpurun_out/$TAG.bench.err || { tail gpurun_out/$TAG.bench.err; exit 2; }
     last gpurun_out/$TAG.bench.json bench value ms_per_step ;;

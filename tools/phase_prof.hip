@@ -3,7 +3,9 @@
 //   (round 4's -DTFHE_SPIN_STATS poll count and the duo form's phases: profiles/r04_spin_stats.txt,
 //   DESIGN.md §4.3d; the duo form now lives in tools/ab/)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DTFHE_PHASE_PROF \
-//         -Izig-tfhe_amd/csrc -o tools/phase_prof tools/phase_prof.hip
+//         -Izig-tfhe_amd/csrc -o tools/bin/phase_prof tools/phase_prof.hip
+// With -DTFHE_PHASE_PROF=2 (-o tools/bin/clock_probe) it is the clock probe instead: no phase
+// marks, each wave's core-clock and 100 MHz tick deltas over its step loop, six launches.
 #include "../zig-tfhe_amd/csrc/tfhe_kernels.hip"
 #include "../zig-tfhe_amd/csrc/tfhe_kernels_whole.hip"
 #include "ab/tfhe_ab_assist_dev.hip"  // "devN": the A/B copy of the assist form, VAR N
@@ -45,7 +47,12 @@ int main(int argc, char **argv) {
     DevTables T{d_twist, d_tw, {tw[2], tw[4], tw[5], tw[6]}};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    for (int rep = 0; rep < 2; rep++) {
+#if TFHE_PHASE_PROF == 2
+    const int reps = 6;  // the clock settles over the first launches
+#else
+    const int reps = 2;
+#endif
+    for (int rep = 0; rep < reps; rep++) {
         unsigned long long z[128] = {0};
 #ifdef TFHE_PHASE_PROF
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), z, sizeof z));
@@ -71,6 +78,17 @@ int main(int argc, char **argv) {
         unsigned long long c[128] = {0};
 #ifdef TFHE_PHASE_PROF
         CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_phase_cycles), sizeof c));
+#endif
+#if TFHE_PHASE_PROF == 2
+        {  // clock probe: [off] core-clock ticks, [off + 1] waves, [off + 2] 100 MHz ticks, per wave group
+            double ticks = 0, waves = 0, real = 0;
+            for (int off = 0; off + 2 < 128; off += 8)
+                if (c[off + 1]) ticks += c[off], waves += c[off + 1], real += c[off + 2];
+            printf("rep %d: %.3f ms (%zu gates, %s); clock probe over %.0f waves: mean wave span %.3f ms "
+                   "(s_memrealtime, 100 MHz), core clock %.4f GHz (s_memtime / s_memrealtime)\n",
+                   rep, ms, B, form, waves, real / waves / 1e5, ticks / real * 0.1);
+            continue;
+        }
 #endif
         if (O.br_form == 3) {  // latency form: per wave, per phase (ticks per step per gate)
             const char *wn0[16] = {"fwd(other)", "barrier1", "sum", "barrier2", "inverse(other)", "barrier3", "tail", "-",

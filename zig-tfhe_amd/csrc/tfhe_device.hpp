@@ -49,11 +49,30 @@ namespace tfhe {
 // defines TFHE_PHASE_PROF, which makes the library an A/B build that
 // tfhe_gpu_create refuses by default): s_memtime deltas per phase, summed per
 // wave and added to g_phase_cycles at the end.  Compiles to nothing otherwise.
+// TFHE_PHASE_PROF=2 is the clock probe: no per-phase marks (they drain the LDS
+// queue and slow the kernel), only the wave's s_memtime (core clock) and
+// s_memrealtime (100 MHz) deltas from start() to flush(), so the kernel runs as
+// unprofiled and the ratio is the clock it held (tools/phase_prof.hip clock).
 struct PhaseProf {
 #ifdef TFHE_PHASE_PROF
     uint64_t last;
     int cur;
     uint64_t acc[16];
+#if TFHE_PHASE_PROF == 2
+    uint64_t real0;
+    DEV void start() {
+        real0 = __builtin_amdgcn_s_memrealtime();
+        last = __builtin_amdgcn_s_memtime();
+    }
+    DEV void mark(int) {}
+    // dst[0] += core-clock ticks, dst[1] += 1 wave, dst[2] += 100 MHz ticks
+    DEV void flush(unsigned long long *dst, int) {
+        const uint64_t now = __builtin_amdgcn_s_memtime(), real = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(dst, (unsigned long long)(now - last));
+        atomicAdd(dst + 1, 1ull);
+        atomicAdd(dst + 2, (unsigned long long)(real - real0));
+    }
+#else
     DEV void start() {
         cur = 0;
         for (int k = 0; k < 16; k++) acc[k] = 0;
@@ -65,6 +84,10 @@ struct PhaseProf {
         last = now;
         cur = k;
     }
+    DEV void flush(unsigned long long *dst, int nq) {
+        for (int q = 0; q < nq; q++) atomicAdd(dst + q, (unsigned long long)acc[q]);
+    }
+#endif
 #else
     DEV void start() {}
     DEV void mark(int) {}
@@ -1106,7 +1129,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate(
         report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
 #ifdef TFHE_PHASE_PROF
         if (ltid % 64 == 0)
-            for (int q = 0; q < 4; q++) atomicAdd(&g_phase_cycles[8 + q], (unsigned long long)lp.acc[q]);
+            lp.flush(g_phase_cycles + 8, 4);
 #endif
         return;
     }
@@ -1224,7 +1247,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate(
     pp.mark(6);
 #ifdef TFHE_PHASE_PROF
     if (t == 0)
-        for (int k = 0; k < 8; k++) atomicAdd(&g_phase_cycles[k], (unsigned long long)pp.acc[k]);
+        pp.flush(g_phase_cycles, 8);
 #endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU) near_tie_flag(P, near, g, valid);

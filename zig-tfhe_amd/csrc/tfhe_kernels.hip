@@ -522,7 +522,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_wide(
     pp.mark(6);
 #ifdef TFHE_PHASE_PROF
     if (t == 0)
-        for (int k = 0; k < 16; k++) atomicAdd(&g_phase_cycles[w * 16 + k], (unsigned long long)pp.acc[k]);
+        pp.flush(g_phase_cycles + w * 16, 16);
 #endif
     if (RC) report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU) near_tie_flag(P, near, g, true);

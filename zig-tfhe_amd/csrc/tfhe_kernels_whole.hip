@@ -216,7 +216,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
         lp.mark(5);
 #ifdef TFHE_PHASE_PROF
         if (t == 0)
-            for (int q = 0; q < 6; q++) atomicAdd(&g_phase_cycles[8 + q], (unsigned long long)lp.acc[q]);
+            lp.flush(g_phase_cycles + 8, 6);
 #endif
         report_wait_failure(P, fail, DEV_ERR_LOADER_WAIT);
         if (FU) near_tie_flag(P, near, g, valid);
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(512, 1) void k_blind_rotate_assist(
     pp.mark(0);
 #ifdef TFHE_PHASE_PROF
     if (t == 0)
-        for (int q = 0; q < 8; q++) atomicAdd(&g_phase_cycles[q], (unsigned long long)pp.acc[q]);
+        pp.flush(g_phase_cycles, 8);
 #endif
     report_wait_failure(P, fail, DEV_ERR_GATE_WAIT);
     if (FU) near_tie_flag(P, near, g, valid);
