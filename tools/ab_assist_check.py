@@ -5,6 +5,7 @@ modes; then timing of one form (BR_FORM=whole|plain|auto).
 Run with TFHE_ALLOW_AB_BUILD=1 TFHE_GPU_LIB=tools/bin/lib_ab.so.
 
     python tools/ab_assist_check.py parity        (FORM=n checks TFHE_OPT_BR_FORM n instead of the whole form)
+    FORM=n python tools/ab_assist_check.py parity_sets   (the 80-bit and UINT4 sets)
     python tools/ab_assist_check.py time STEPS
 """
 import os
@@ -68,6 +69,32 @@ def parity():
     c.close()
 
 
+def parity_sets():
+    """FORM=n at the 80-bit and UINT4 sets (UINT4: reference trees, L = 1): the oracle on 3
+    rotations, and the product's default form (auto) on 64, every output word."""
+    from oracle import Oracle, params
+    form = int(os.environ["FORM"])
+    o = Oracle()
+    for name in ("80", "uint4"):
+        p = params(name)
+        k0, k1 = o.secret_key(p, 42)
+        ck = o.cloud_key(p, 43, k0, k1)
+        c = tfhe_amd.Context(name, 0)
+        c.load_cloud_key(ck.offset, ck.testvec, ck.bk, ck.ksk)
+        g = np.random.default_rng(7)
+        cts = u32rand(g, 64, p.n + 1)
+        want = np.array([o.blind_rotate(p, t, ck.testvec, ck.bk, ck.offset) for t in cts[:3]])
+        ref = c.blind_rotate_batch(cts)
+        auto = c.last_kernels()
+        with c.options(br_form=form):
+            got = c.blind_rotate_batch(cts)
+            kern = c.last_kernels()
+        assert np.array_equal(got[:3], want), f"{name}: form {form} != oracle"
+        assert np.array_equal(got, ref), f"{name}: form {form} != {auto}"
+        print(f"{name}: {kern}: oracle on 3, the default form ({auto}) on 64: identical")
+        c.close()
+
+
 def timing(steps):
     c = tfhe_amd.Context("128", 0)
     sk, _ = c.keygen(42, 43)
@@ -100,5 +127,7 @@ def timing(steps):
 if __name__ == "__main__":
     if sys.argv[1] == "parity":
         parity()
+    elif sys.argv[1] == "parity_sets":
+        parity_sets()
     else:
         timing(int(sys.argv[2]))
