@@ -4,7 +4,7 @@ batches of B gates with uniformly random ciphertext words (every rotation
 uniform) and random gate ops, device-resident; every output word compared.
 Development evidence for DESIGN.md §6.1 (profiles/r05_soak_fused.json).
 
-    python tools/soak_fused.py [PARAMS=128] [BATCHES=256] [B=4096]
+    python tools/soak_fused.py [PARAMS=128] [BATCHES=256] [B=4096] [SEED=2024]
 """
 import json
 import os
@@ -23,13 +23,14 @@ def main():
     pname = sys.argv[1] if len(sys.argv) > 1 else "128"
     batches = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     B = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+    seed = int(sys.argv[4]) if len(sys.argv) > 4 else 2024
     dev = torch.device("cuda", 0)
     c = tfhe_amd.Context(pname, 0)
     c.keygen(42, 43)
     n1 = c.params.n + 1
     c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     gen = torch.Generator(device=dev)
-    gen.manual_seed(2024)
+    gen.manual_seed(seed)
     t_a = torch.empty((B, n1), dtype=torch.int32, device=dev)
     t_b = torch.empty_like(t_a)
     o_f = torch.empty_like(t_a)
@@ -55,7 +56,7 @@ def main():
     torch.cuda.synchronize(dev)
     c.sync()
     rec = {"params": pname, "gates": batches * B, "batches": batches, "batch": B,
-           "inputs": "uniformly random ciphertext words (torch generator seed 2024), ops uniform over the ten gates",
+           "inputs": f"uniformly random ciphertext words (torch generator seed {seed}), ops uniform over the ten gates",
            "gates_with_differing_words": differ, "near_tie_items_recomputed": c.near_tie_items() - ties0,
            "kernels": kernels, "build_id": tfhe_amd.build_id(), "seconds": round(time.time() - t0, 1)}
     print(json.dumps(rec))
