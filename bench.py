@@ -667,12 +667,13 @@ def main():
     rank, world, local = tdist.env_rank_world()
     if world != args.gpus:
         raise SystemExit(f"bench.py: {world} rank(s) launched but --gpus {args.gpus}")
-    if world > 1:
-        dist.init_process_group(args.dist_backend)  # nccl = RCCL over xGMI
     # one rank per GPU; --dist-backend gloo with more ranks than GPUs only
-    # rehearses the multi-rank path (ranks then share a device)
+    # rehearses the multi-rank path (ranks then share a device).  The device is set
+    # before the process group exists, so RCCL's communicator binds this rank's GPU.
     device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group(args.dist_backend)  # nccl = RCCL over xGMI
     if args.workload != "nand":
         run_workload(args, rank, world, device)
         if world > 1:
