@@ -359,8 +359,10 @@ int h2d(tfhe_gpu_ctx *c, DevBuf &buf, const void *src, size_t bytes) {
     if (c->stage_used + need > c->stage_in_bytes) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->stage_used = 0;
-        rc = ensure_stage(c, c->stage_in, c->stage_in_bytes, std::max(need, 2 * c->stage_in_bytes));
-        if (rc) return rc;
+        if (need > c->stage_in_bytes) {  // grow (doubling) only when one copy does not fit the empty arena
+            rc = ensure_stage(c, c->stage_in, c->stage_in_bytes, std::max(need, 2 * c->stage_in_bytes));
+            if (rc) return rc;
+        }
     }
     char *p = c->stage_in + c->stage_used;
     std::memcpy(p, src, bytes);
