@@ -101,9 +101,11 @@ def f64_ops_per_cmux(L: int, fused: bool = False) -> int:
 
 
 VALU_F64_PEAK = 256 * 4 * 16 * 2.4e9  # f64 VALU lane-ops/s: 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz (78.6 TF FMA spec / 2)
-# measured with tools/isa_rate.hip (profiles/r01_isa_rate.txt): independent v_add_f64 / v_mul_f64
-# at 4 waves per SIMD issue every 2.01 ns per SIMD -> 1024 SIMDs x 64 lanes / 2.01 ns
-VALU_F64_SUSTAINED = 1024 * 64 / 2.01e-9
+# measured with tools/isa_rate.hip in core-clock cycles (profiles/r06o_isa_rate_cycles.txt; the
+# round-1 ns figures ran at an unknown, ramping clock): independent v_fmac_f64, 8 chains per wave,
+# issue every 4.41 cycles per SIMD at 4 waves per SIMD, 4.84 at 2 and 5.99 at 1
+ISSUE_CYCLES_F64 = {4: 4.41, 2: 4.84, 1: 5.99}
+VALU_F64_SUSTAINED = 1024 * 64 * 2.4e9 / ISSUE_CYCLES_F64[4]  # at 2.4 GHz, as VALU_F64_PEAK
 
 
 def host_cpu_info() -> dict:
@@ -257,19 +259,25 @@ def rooflines(p, B, params, br_avg_s, kernel):
         if f64_insts:
             roof["pmc"]["valu_f64_frac_from_pmc"] = round(f64_insts * 64 / br_avg_s / VALU_F64_PEAK, 4)
         # what binds the step: the SIMD's VALU issue for the item as a whole (gate
-        # and loader waves, f64 and integer), measured as wave-instructions per SIMD per launch
-        # (PMC SQ_INSTS_VALU / 1,024 SIMDs) against the sustained issue interval of tools/isa_rate.hip
-        # (2.01 ns per wave-instruction per SIMD for v_add/v_mul_f64 at 4 waves per SIMD; 2.14 ns at 2)
+        # and loader waves, f64 and integer), as core-clock cycles per VALU wave-instruction per SIMD
+        # (the kernel's cycles per launch / (PMC SQ_INSTS_VALU / 1,024 SIMDs)) against the issue
+        # interval tools/isa_rate.hip measures in cycles (ISSUE_CYCLES_F64); both sides in cycles, so
+        # the clock the run held cancels
         insts = pmc.get("raw_per_launch", {}).get("SQ_INSTS_VALU")
         if insts:
-            ns = br_avg_s * 1e9 / (insts / (256 * 4))
-            roof["valu_issue"] = {"ns_per_valu_inst_per_simd": round(ns, 3), "peak_ns_4_waves": 2.01,
-                                  "peak_ns_2_waves": 2.14, "frac": round(2.01 / ns, 4),
+            per_simd = insts / (256 * 4)
+            cyc = probe["cycles_per_launch"] / per_simd if probe else br_avg_s * 2.4e9 / per_simd
+            roof["valu_issue"] = {"cycles_per_valu_inst_per_simd": round(cyc, 3),
+                                  "peak_cycles_4_waves": ISSUE_CYCLES_F64[4], "peak_cycles_2_waves": ISSUE_CYCLES_F64[2],
+                                  "peak_cycles_1_wave": ISSUE_CYCLES_F64[1], "frac": round(ISSUE_CYCLES_F64[4] / cyc, 4),
+                                  "frac_2_waves": round(ISSUE_CYCLES_F64[2] / cyc, 4),
                                   "valu_insts_per_item_per_cmux": pmc.get("valu_insts_per_item_per_cmux"),
-                                  "note": "issue interval achieved vs the measured sustained f64 VALU interval; "
-                                          "the kernel runs 2 waves per SIMD (gate + loader)",
+                                  "note": "cycles per VALU instruction per SIMD achieved vs the measured f64 issue interval "
+                                          "(profiles/r06o_isa_rate_cycles.txt); the kernel runs 2 waves per SIMD "
+                                          "(gate + loader), and one wave alone issues f64 every 5.99 cycles",
                                   "provenance": "SQ_INSTS_VALU " + record_provenance(PMC_PATH, pmc)
-                                                + "; kernel time in-run (HIP events)"}
+                                                + ("; cycles per launch from the clock-probe record" if probe
+                                                   else "; cycles = in-run kernel time x 2.4 GHz (no clock-probe record)")}
         # the DRAM side of the same kernel: measured bytes per launch / kernel time / HBM peak
         roof["dram"] = {"achieved_gbs": round(pmc["hbm_bytes_per_launch"] / br_avg_s / 1e9, 1),
                         "peak_gbs": HBM_PEAK_BPS / 1e9,

@@ -64,10 +64,13 @@ def test_roofline_from_committed_records(monkeypatch):
     assert roof["kernel_avg_ms_rocprof"] == pytest.approx(avg_ms, abs=1e-3)
     assert "committed record" in roof["rocprof"]["provenance"] and "committed record" in roof["pmc"]["provenance"]
     assert roof["frac_rocprof"] == pytest.approx(ops / (avg_ms / 1e3) / bench.VALU_F64_PEAK, abs=1e-4)
-    # VALU issue: wave-instructions per SIMD per launch against the kernel time
-    ns = kernel_s * 1e9 / (pmc["raw_per_launch"]["SQ_INSTS_VALU"] / 1024)
-    assert roof["valu_issue"]["ns_per_valu_inst_per_simd"] == pytest.approx(ns, abs=1e-3)
-    assert roof["valu_issue"]["frac"] == pytest.approx(2.01 / ns, abs=1e-4)
+    # VALU issue in core-clock cycles: the kernel's cycles per launch (clock-probe record) per VALU
+    # wave-instruction per SIMD, against the measured f64 issue interval at 4 waves per SIMD
+    probe = json.load(open(bench.CLOCK_PROBE_PATH))
+    cyc = probe["cycles_per_launch"] / (pmc["raw_per_launch"]["SQ_INSTS_VALU"] / 1024)
+    assert roof["valu_issue"]["cycles_per_valu_inst_per_simd"] == pytest.approx(cyc, abs=1e-3)
+    assert roof["valu_issue"]["frac"] == pytest.approx(4.41 / cyc, abs=1e-4)
+    assert 0.5 < roof["valu_issue"]["frac"] < 1.0
     # DRAM side: measured bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, KB x1024)
     raw = pmc["raw_per_launch"]
     assert roof["traffic"] == int(raw["FETCH_SIZE"] * 1024 * 2 + raw["WRITE_SIZE"] * 1024)

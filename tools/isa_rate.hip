@@ -1,7 +1,10 @@
 // Development micro-benchmark: issue rate of the VALU instructions the
 // blind-rotation kernel uses, as a function of waves per SIMD (1, 2, 4) and of
 // independent chains per wave (4, 8, 16).  Event-timed over all 256 CUs; prints
-// ns per wave-instruction per SIMD (lower = better).
+// ns per wave-instruction per SIMD (lower = better) and, since round 6, the core
+// clock the waves held (s_memtime over s_memrealtime at 100 MHz, as the clock probe)
+// and cycles per wave-instruction per SIMD, which do not depend on that clock.
+// Each configuration runs 8 warm launches first (the clock ramps over ~40 ms).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Wno-unused-value -o tools/bin/isa_rate tools/isa_rate.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -32,7 +35,7 @@ static const char *NAMES[] = {"v_add_f64", "v_mul_f64", "v_add_u32", "v_cvt_f64_
                               "v_fma_f64", "v_fmac_f64", "v_fma_f64 a*a+c", "v_fma_f64 sgpr", "v_add_f64 sgpr"};
 
 template <int OP, int C>
-__global__ void k_rate(double *out, int iters, double sc) {
+__global__ void k_rate(double *out, int iters, double sc, unsigned long long *clk) {
     double a[16], b[16];
     unsigned u[16];
     for (int i = 0; i < 16; i++) {
@@ -40,11 +43,17 @@ __global__ void k_rate(double *out, int iters, double sc) {
         b[i] = 1.0 + i * 1e-3;
         u[i] = threadIdx.x + i;
     }
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int k = 0; k < iters; k++) {
         body<OP, C>(a, b, u, sc);
         body<OP, C>(a, b, u, sc);
         body<OP, C>(a, b, u, sc);
         body<OP, C>(a, b, u, sc);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {  // per wave: core-clock and 100 MHz ticks of its loop
+        atomicAdd(clk, t1 - t0);
+        atomicAdd(clk + 1, r1 - r0);
     }
     double s = 0;
     for (int i = 0; i < 16; i++) s += a[i] + u[i];
@@ -52,51 +61,58 @@ __global__ void k_rate(double *out, int iters, double sc) {
 }
 
 template <int OP, int C>
-void run(double *out, int wps) {
+void run(double *out, unsigned long long *clk, int wps) {
     const int iters = 16000 / C, blocks = 256, threads = 256 * wps;
-    hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, 10, 1.0000001);
+    for (int w = 0; w < 8; w++)  // warm launches: the clock settles
+        hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, iters, 1.0000001, clk);
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     float best = 1e9;
+    double ghz = 0;
     for (int r = 0; r < 3; r++) {
+        hipMemset(clk, 0, 2 * sizeof(unsigned long long));
         hipEventRecord(e0);
-        hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, iters, 1.0000001);
+        hipLaunchKernelGGL((k_rate<OP, C>), dim3(blocks), dim3(threads), 0, 0, out, iters, 1.0000001, clk);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
         hipEventElapsedTime(&ms, e0, e1);
-        best = ms < best ? ms : best;
+        unsigned long long c[2];
+        hipMemcpy(c, clk, sizeof c, hipMemcpyDeviceToHost);
+        if (ms < best) best = ms, ghz = c[1] ? (double)c[0] / (double)c[1] * 0.1 : 0;
     }
     const double ninst = (double)iters * 4 * C * (OP == 4 ? 2 : 1) * wps;  // per SIMD
-    printf("%-16s chains %2d waves/SIMD %d  %.3f ms  %.3f ns/inst/SIMD\n", NAMES[OP], C, wps, best,
-           best * 1e6 / ninst);
+    printf("%-16s chains %2d waves/SIMD %d  %.3f ms  %.3f ns/inst/SIMD  clock %.3f GHz  %.2f cycles/inst/SIMD\n",
+           NAMES[OP], C, wps, best, best * 1e6 / ninst, ghz, best * 1e6 / ninst * ghz);
 }
 
 template <int OP>
-void run_op(double *out) {
-    run<OP, 4>(out, 1);
-    run<OP, 8>(out, 1);
-    run<OP, 16>(out, 1);
-    run<OP, 8>(out, 2);
-    run<OP, 16>(out, 2);
-    run<OP, 8>(out, 4);
+void run_op(double *out, unsigned long long *clk) {
+    run<OP, 4>(out, clk, 1);
+    run<OP, 8>(out, clk, 1);
+    run<OP, 16>(out, clk, 1);
+    run<OP, 8>(out, clk, 2);
+    run<OP, 16>(out, clk, 2);
+    run<OP, 8>(out, clk, 4);
 }
 
 int main() {
     double *out;
+    unsigned long long *clk;
     hipMalloc(&out, 256 * 1024 * sizeof(double));
-    run_op<0>(out);
-    run_op<1>(out);
-    run_op<2>(out);
-    run_op<3>(out);
-    run_op<4>(out);
-    run_op<5>(out);
-    run_op<6>(out);
-    run_op<7>(out);
-    run_op<8>(out);
-    run_op<9>(out);
-    run_op<10>(out);
+    hipMalloc(&clk, 2 * sizeof(unsigned long long));
+    run_op<0>(out, clk);
+    run_op<1>(out, clk);
+    run_op<2>(out, clk);
+    run_op<3>(out, clk);
+    run_op<4>(out, clk);
+    run_op<5>(out, clk);
+    run_op<6>(out, clk);
+    run_op<7>(out, clk);
+    run_op<8>(out, clk);
+    run_op<9>(out, clk);
+    run_op<10>(out, clk);
     hipDeviceSynchronize();
     return 0;
 }
