@@ -115,3 +115,20 @@ def test_clock_falls_back_to_the_pmc_pass(monkeypatch, tmp_path):
     monkeypatch.setattr(bench, "CLOCK_PROBE_PATH", str(tmp_path / "none.json"))
     roof, _ = bench.rooflines(tfhe_amd.make_params("128"), 1024, "128", 5.97e-3, "k_blind_rotate_assist<true> (fused)")
     assert roof["clock_ghz"] == pmc["clock_ghz"] and "clock_ghz_pmc_pass" not in roof
+
+
+def test_clock_probe_record_from_its_log():
+    """tools/clock_probe_record.py turns the committed probe log back into the committed record's
+    cycle counts (the numbers bench.py divides by its kernel time)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("cpr", os.path.join(ROOT, "tools", "clock_probe_record.py"))
+    cpr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cpr)
+    probe = json.load(open(bench.CLOCK_PROBE_PATH))
+    reps = cpr.parse(open(os.path.join(ROOT, probe["source"])).read())
+    assert len(reps) == 6 and all(r["batch"] == 1024 and r["waves"] == 2048 for r in reps)
+    rec = cpr.record(reps, probe["source"], probe["kernel_build_id"])
+    for k in ("cycles_per_launch", "cycles_per_launch_spread", "cycles_per_wave_span", "cycles_per_wave_span_spread"):
+        assert rec[k] == probe[k], k
+    with pytest.raises(SystemExit):
+        cpr.record(reps[:3], "x", "y")
